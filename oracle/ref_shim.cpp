@@ -1,0 +1,133 @@
+// ref_shim.cpp -- extern "C" wrappers around the REFERENCE library compiled
+// from its own sources under /root/reference (oracle/Makefile, target
+// `ref`).  TEST INFRASTRUCTURE ONLY: used to generate the golden fixtures
+// (oracle/gen_golden.cpp) and as bench.py's cpu_baseline (kind "reference").
+// The output library lives in oracle/_ref/ (git-ignored).
+//
+// Two entry families:
+//   tpref_s_*  -> turbopfor::scalar::*   (src/scalar, the bit-exact oracle)
+//   tpref_d_*  -> turbopfor::*           (src/dispatch.cpp; AVX2/SSE4.2 paths
+//                                         when built with ENABLE_AVX2/SSE42)
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+#include <chrono>
+
+#include "turbopfor.h"           // /root/reference/include
+#include "scalar/p4_scalar.h"    // /root/reference/src
+
+extern "C" {
+
+#define W32ENC(name, ns, fn) \
+    uint8_t * name(uint32_t * in, unsigned n, uint8_t * out) { return ns::fn(in, n, out); }
+#define W32D1ENC(name, ns, fn) \
+    uint8_t * name(uint32_t * in, unsigned n, uint8_t * out, uint32_t s) { return ns::fn(in, n, out, s); }
+#define W32DEC(name, ns, fn) \
+    const uint8_t * name(const uint8_t * in, unsigned n, uint32_t * out) { return ns::fn(in, n, out); }
+#define W32D1DEC(name, ns, fn) \
+    const uint8_t * name(const uint8_t * in, unsigned n, uint32_t * out, uint32_t s) { return ns::fn(in, n, out, s); }
+#define W64ENC(name, ns, fn) \
+    uint8_t * name(uint64_t * in, unsigned n, uint8_t * out) { return ns::fn(in, n, out); }
+#define W64D1ENC(name, ns, fn) \
+    uint8_t * name(uint64_t * in, unsigned n, uint8_t * out, uint64_t s) { return ns::fn(in, n, out, s); }
+#define W64DEC(name, ns, fn) \
+    const uint8_t * name(const uint8_t * in, unsigned n, uint64_t * out) { return ns::fn(in, n, out); }
+#define W64D1DEC(name, ns, fn) \
+    const uint8_t * name(const uint8_t * in, unsigned n, uint64_t * out, uint64_t s) { return ns::fn(in, n, out, s); }
+
+#define FAMILY(prefix, ns)                                   \
+    W32ENC(prefix##p4enc32, ns, p4Enc32)                     \
+    W32D1ENC(prefix##p4d1enc32, ns, p4D1Enc32)               \
+    W32DEC(prefix##p4dec32, ns, p4Dec32)                     \
+    W32D1DEC(prefix##p4d1dec32, ns, p4D1Dec32)               \
+    W32ENC(prefix##p4enc128v32, ns, p4Enc128v32)             \
+    W32D1ENC(prefix##p4d1enc128v32, ns, p4D1Enc128v32)       \
+    W32DEC(prefix##p4dec128v32, ns, p4Dec128v32)             \
+    W32D1DEC(prefix##p4d1dec128v32, ns, p4D1Dec128v32)       \
+    W32ENC(prefix##p4enc256v32, ns, p4Enc256v32)             \
+    W32D1ENC(prefix##p4d1enc256v32, ns, p4D1Enc256v32)       \
+    W32DEC(prefix##p4dec256v32, ns, p4Dec256v32)             \
+    W32D1DEC(prefix##p4d1dec256v32, ns, p4D1Dec256v32)       \
+    W64ENC(prefix##p4enc128v64, ns, p4Enc128v64)             \
+    W64D1ENC(prefix##p4d1enc128v64, ns, p4D1Enc128v64)       \
+    W64DEC(prefix##p4dec128v64, ns, p4Dec128v64)             \
+    W64D1DEC(prefix##p4d1dec128v64, ns, p4D1Dec128v64)       \
+    W64ENC(prefix##p4enc256v64, ns, p4Enc256v64)             \
+    W64D1ENC(prefix##p4d1enc256v64, ns, p4D1Enc256v64)       \
+    W64DEC(prefix##p4dec256v64, ns, p4Dec256v64)             \
+    W64D1DEC(prefix##p4d1dec256v64, ns, p4D1Dec256v64)
+
+FAMILY(tpref_s_, turbopfor::scalar)
+FAMILY(tpref_d_, turbopfor)
+
+// Streaming decode of nblocks consecutive 256v32 blocks (block i at
+// in+off[i]) on nthreads std::threads, each a contiguous block range.
+// use_dispatch=1 -> turbopfor::p4Dec256v32 (AVX2 path), 0 -> scalar.
+// Returns wall seconds of the parallel region.
+double tpref_dec256v32_stream_mt(const uint8_t * in, const uint64_t * off, uint64_t nblocks, uint32_t * out,
+                                 int nthreads, int use_dispatch, int d1)
+{
+    if (nthreads < 1)
+        nthreads = 1;
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t)
+    {
+        uint64_t lo = nblocks * (uint64_t)t / (uint64_t)nthreads;
+        uint64_t hi = nblocks * (uint64_t)(t + 1) / (uint64_t)nthreads;
+        th.emplace_back([=] {
+            for (uint64_t i = lo; i < hi; ++i)
+            {
+                uint32_t * o = out + i * 256u;
+                if (d1)
+                {
+                    uint32_t st = i ? 0u : 0u;
+                    if (use_dispatch)
+                        turbopfor::p4D1Dec256v32(in + off[i], 256u, o, st);
+                    else
+                        turbopfor::scalar::p4D1Dec256v32(in + off[i], 256u, o, st);
+                }
+                else if (use_dispatch)
+                    turbopfor::p4Dec256v32(in + off[i], 256u, o);
+                else
+                    turbopfor::scalar::p4Dec256v32(in + off[i], 256u, o);
+            }
+        });
+    }
+    for (auto & x : th)
+        x.join();
+    auto t1 = std::chrono::steady_clock::now();
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// ab_test methodology (benchmarks/ab_test.cpp:553-701): one block decoded in
+// an L1-hot loop, `iters` iterations per chunk, best of `runs` runs.  Returns
+// best seconds per decode call.
+double tpref_abtest_dec256v32(const uint8_t * blk, unsigned iters, unsigned runs, int use_dispatch)
+{
+    alignas(64) uint32_t out[256 + 64];
+    volatile uint32_t sink = 0;
+    for (unsigned w = 0; w < 1000; ++w)
+        use_dispatch ? (void)turbopfor::p4Dec256v32(blk, 256u, out) : (void)turbopfor::scalar::p4Dec256v32(blk, 256u, out);
+    double best = 1e30;
+    for (unsigned r = 0; r < runs; ++r)
+    {
+        auto t0 = std::chrono::steady_clock::now();
+        for (unsigned i = 0; i < iters; ++i)
+        {
+            if (use_dispatch)
+                turbopfor::p4Dec256v32(blk, 256u, out);
+            else
+                turbopfor::scalar::p4Dec256v32(blk, 256u, out);
+            sink = sink + out[i & 255u];
+        }
+        auto t1 = std::chrono::steady_clock::now();
+        double s = std::chrono::duration<double>(t1 - t0).count() / iters;
+        if (s < best)
+            best = s;
+    }
+    return best;
+}
+
+} // extern "C"
