@@ -1,0 +1,74 @@
+/*
+ * turbopfor_gpu.h -- C-ABI of the MI355X (gfx950) P4 codec: batched device
+ * entry points.  Plain C types only (no HIP/torch types): `stream` is a
+ * hipStream_t passed as void* (NULL = the default stream).  All pointers named
+ * d_* are device pointers; inputs are expected to be resident in HBM.
+ *
+ * Layout contract for the batched 256v32 / 256v64 formats:
+ *   - the packed stream is the reference's per-block encodings laid end to
+ *     end, exactly as the reference's callers chain them with the returned end
+ *     pointer (README.md:108-123);
+ *   - d_off[0..nblocks] are byte offsets of each block (d_off[nblocks] = end);
+ *     the reference has no offsets (block sizes are implicit), so the batch
+ *     encoders produce them and tpf_scan_blocks* recovers them from a legacy
+ *     stream;
+ *   - decoded values are nblocks * 256 contiguous integers.
+ * No device-side slack is required: all device reads are bounds-checked
+ * against in_bytes.
+ *
+ * Return value: TPF_OK (0) or a negative TPF_E* code; tpf_last_error()
+ * returns a thread-local message for the last failure.
+ */
+#ifndef TURBOPFOR_GPU_H
+#define TURBOPFOR_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TPF_OK 0
+#define TPF_EINVAL (-1)  /* bad argument */
+#define TPF_EHIP (-2)    /* HIP runtime error (see tpf_last_error) */
+#define TPF_ENODEV (-3)  /* no HIP device: the library has no CPU fallback */
+#define TPF_ECORRUPT (-4) /* a block's parsed length disagrees with its offsets */
+
+const char *tpf_last_error(void);
+int tpf_device_count(void);
+
+/* ---- 256v32 decode (hot path) ------------------------------------------
+ * Replaces per-block turbopfor::p4Dec256v32 (reference include/turbopfor.h:39,
+ * src/dispatch.cpp:88-95).  d_err (optional, may be NULL): receives the index
+ * of the first block whose parsed byte length differs from
+ * d_off[i+1]-d_off[i], or UINT64_MAX when every block is consistent. */
+int tpf_p4dec256v32_batch(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks,
+                          uint32_t *d_out, uint64_t *d_err, void *stream);
+
+/* Replaces turbopfor::p4D1Dec256v32 (include/turbopfor.h:42, dispatch.cpp:97-104):
+ * block i is decoded with start d_starts[i] (the value preceding the block). */
+int tpf_p4d1dec256v32_batch(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks,
+                            uint32_t *d_out, const uint32_t *d_starts, uint64_t *d_err, void *stream);
+
+/* ---- 256v32 encode ---------------------------------------------------
+ * Replaces turbopfor::p4Enc256v32 (include/turbopfor.h:33, dispatch.cpp:70-77)
+ * and p4D1Enc256v32 (:36, dispatch.cpp:79-86) for nblocks blocks of 256
+ * values (d_in: nblocks*256 u32).  Writes the blocks end to end into d_out
+ * (capacity out_cap bytes; tpf_p4enc256v32_bound(nblocks) always suffices)
+ * and their byte offsets into d_off[0..nblocks] (d_off[nblocks] = total).
+ * d_ws: device workspace of tpf_p4enc256v32_workspace_size(nblocks) bytes.
+ * D1: d_starts[i] is the value preceding block i; with d_starts == NULL the
+ * blocks are one chained posting list: block 0 starts from start0 and block
+ * i>0 from the last input value of block i-1. */
+uint64_t tpf_p4enc256v32_bound(uint64_t nblocks);
+size_t tpf_p4enc256v32_workspace_size(uint64_t nblocks);
+int tpf_p4enc256v32_batch(const uint32_t *d_in, uint64_t nblocks, uint8_t *d_out, uint64_t out_cap, uint64_t *d_off,
+                          void *d_ws, size_t ws_bytes, void *stream);
+int tpf_p4d1enc256v32_batch(const uint32_t *d_in, uint64_t nblocks, const uint32_t *d_starts, uint32_t start0,
+                            uint8_t *d_out, uint64_t out_cap, uint64_t *d_off, void *d_ws, size_t ws_bytes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,71 @@
+"""GPU parity of the 256v32 batch encoder (p4Enc256v32 / p4D1Enc256v32):
+byte-exact against the golden fixtures (reference src/scalar outputs) and the
+CPU restatement, plus encode->decode round trips at larger sizes."""
+import numpy as np
+import pytest
+
+import datagen
+import golden_io
+import oracle_lib
+
+torch = pytest.importorskip("torch")
+tpf = pytest.importorskip("turbopfor_amd")
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def dev_u32(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32).view(np.int32)).to(DEV)
+
+
+def test_golden_256v32_encode():
+    recs = [r for r in golden_io.load("g256v32.bin") if r.n == 256 and not r.decode_only]
+    for d1 in (False, True):
+        sel = [r for r in recs if r.d1 == d1]
+        vals = np.stack([r.values for r in sel])
+        starts = dev_u32(np.array([r.start for r in sel], dtype=np.uint32)) if d1 else None
+        packed, offs = tpf.enc256v32(dev_u32(vals), d1=d1, starts=starts)
+        packed = packed.cpu().numpy().tobytes()
+        offs = offs.cpu().numpy()
+        assert offs[-1] == sum(len(r.enc) for r in sel)
+        for i, r in enumerate(sel):
+            assert packed[offs[i]:offs[i + 1]] == r.enc, f"golden d1={d1} record {i}"
+
+
+@pytest.mark.parametrize("exc", [0, 5, 10, 25])
+def test_c2_encode_vs_oracle(exc):
+    blocks = np.concatenate([datagen.c2_blocks(48, bw, exc, seed=exc + 3) for bw in range(1, 33)])
+    exp_packed, exp_off = oracle_lib.enc256v32_batch(blocks)
+    packed, offs = tpf.enc256v32(dev_u32(blocks))
+    np.testing.assert_array_equal(offs.cpu().numpy().astype(np.uint64), exp_off)
+    np.testing.assert_array_equal(packed.cpu().numpy(), exp_packed)
+
+
+def test_c3_d1_encode_chained_and_starts():
+    vals, starts = datagen.c3_postings(2000)
+    exp_packed, exp_off = oracle_lib.enc256v32_batch(vals, starts=starts)
+    p1, o1 = tpf.enc256v32(dev_u32(vals), d1=True, starts=dev_u32(starts))
+    np.testing.assert_array_equal(p1.cpu().numpy(), exp_packed)
+    p2, o2 = tpf.enc256v32(dev_u32(vals), d1=True, start0=0)  # chained: same starts
+    np.testing.assert_array_equal(p2.cpu().numpy(), exp_packed)
+    np.testing.assert_array_equal(o2.cpu().numpy().astype(np.uint64), exp_off)
+
+
+def test_roundtrip_large_mixed():
+    """Size-independent property at scale: decode(encode(x)) == x."""
+    g = torch.Generator(device=DEV)
+    g.manual_seed(1234)
+    nb = 200_000
+    bw = torch.randint(1, 33, (nb, 1), device=DEV, generator=g)
+    raw = torch.randint(0, 1 << 62, (nb, 256), device=DEV, generator=g, dtype=torch.int64)
+    base = raw & ((1 << bw) - 1)
+    exc = (torch.rand((nb, 256), device=DEV, generator=g) < 0.1) & (bw <= 28)
+    vals = torch.where(exc, raw >> 30, base).to(torch.int64) & 0xFFFFFFFF
+    vals = (vals - ((vals >> 31) << 32)).to(torch.int32)  # uint32 bit pattern as int32
+    packed, offs = tpf.enc256v32(vals)
+    err = torch.zeros(1, dtype=torch.int64, device=DEV)
+    out = tpf.dec256v32(packed, offs, nb, err=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == -1
+    assert torch.equal(out, vals.view(nb, 256))

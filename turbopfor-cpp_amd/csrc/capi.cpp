@@ -1,0 +1,142 @@
+// capi.cpp -- extern "C" entry points of include/turbopfor_gpu.h.
+// Argument checking, error reporting and launch sizing; the kernels live in
+// the *.hip files.  There is deliberately no CPU fallback: without a HIP
+// device every entry point fails with TPF_ENODEV.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "../../include/turbopfor_gpu.h"
+#include "tpf_kernels.h"
+
+namespace
+{
+thread_local std::string g_err;
+
+int fail(int code, const std::string & msg)
+{
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char * where)
+{
+    return fail(TPF_EHIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+int check_device()
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return fail(TPF_ENODEV, "no HIP device visible (turbopfor_amd has no CPU fallback)");
+    return TPF_OK;
+}
+
+// d_err handling: init to UINT64_MAX before the kernel.
+int prep_err(uint64_t * d_err, hipStream_t s)
+{
+    if (!d_err)
+        return TPF_OK;
+    hipError_t e = hipMemsetAsync(d_err, 0xFF, sizeof(uint64_t), s);
+    return e == hipSuccess ? TPF_OK : hip_fail(e, "hipMemsetAsync(d_err)");
+}
+} // namespace
+
+namespace tpf
+{
+uint64_t grid_cap(hipStream_t, uint32_t per_cu)
+{
+    static int cus[64] = {0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64)
+        dev = 0;
+    if (cus[dev] == 0)
+    {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        cus[dev] = n;
+    }
+    return static_cast<uint64_t>(cus[dev]) * per_cu;
+}
+} // namespace tpf
+
+extern "C" {
+
+const char * tpf_last_error(void) { return g_err.c_str(); }
+
+int tpf_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess)
+        return 0;
+    return n;
+}
+
+int tpf_p4dec256v32_batch(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nblocks, uint32_t * d_out,
+                          uint64_t * d_err, void * stream)
+{
+    if (int rc = check_device())
+        return rc;
+    if (nblocks && (!d_in || !d_off || !d_out))
+        return fail(TPF_EINVAL, "tpf_p4dec256v32_batch: null pointer");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (int rc = prep_err(d_err, s))
+        return rc;
+    hipError_t e = tpf::launch_dec256v32(d_in, in_bytes, d_off, nblocks, d_out, nullptr,
+                                         reinterpret_cast<unsigned long long *>(d_err), s);
+    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_p4dec256v32_batch");
+}
+
+int tpf_p4d1dec256v32_batch(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nblocks, uint32_t * d_out,
+                            const uint32_t * d_starts, uint64_t * d_err, void * stream)
+{
+    if (int rc = check_device())
+        return rc;
+    if (nblocks && (!d_in || !d_off || !d_out || !d_starts))
+        return fail(TPF_EINVAL, "tpf_p4d1dec256v32_batch: null pointer");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (int rc = prep_err(d_err, s))
+        return rc;
+    hipError_t e = tpf::launch_dec256v32(d_in, in_bytes, d_off, nblocks, d_out, d_starts,
+                                         reinterpret_cast<unsigned long long *>(d_err), s);
+    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_p4d1dec256v32_batch");
+}
+
+uint64_t tpf_p4enc256v32_bound(uint64_t nblocks) { return nblocks * 1800u + 64u; }
+
+size_t tpf_p4enc256v32_workspace_size(uint64_t nblocks) { return tpf::enc256v32_workspace(nblocks); }
+
+static int enc256v32_common(const uint32_t * d_in, uint64_t nblocks, const uint32_t * d_starts, uint32_t start0, bool d1,
+                            uint8_t * d_out, uint64_t out_cap, uint64_t * d_off, void * d_ws, size_t ws_bytes, void * stream,
+                            const char * name)
+{
+    if (int rc = check_device())
+        return rc;
+    if (!d_off || (nblocks && (!d_in || !d_out || !d_ws)))
+        return fail(TPF_EINVAL, std::string(name) + ": null pointer");
+    if (ws_bytes < tpf::enc256v32_workspace(nblocks))
+        return fail(TPF_EINVAL, std::string(name) + ": workspace too small");
+    hipError_t e = tpf::launch_enc256v32(d_in, nblocks, d_starts, start0, d1, d_out, out_cap, d_off, d_ws, ws_bytes,
+                                         static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TPF_OK : hip_fail(e, name);
+}
+
+int tpf_p4enc256v32_batch(const uint32_t * d_in, uint64_t nblocks, uint8_t * d_out, uint64_t out_cap, uint64_t * d_off, void * d_ws,
+                          size_t ws_bytes, void * stream)
+{
+    return enc256v32_common(d_in, nblocks, nullptr, 0, false, d_out, out_cap, d_off, d_ws, ws_bytes, stream, "tpf_p4enc256v32_batch");
+}
+
+int tpf_p4d1enc256v32_batch(const uint32_t * d_in, uint64_t nblocks, const uint32_t * d_starts, uint32_t start0, uint8_t * d_out,
+                            uint64_t out_cap, uint64_t * d_off, void * d_ws, size_t ws_bytes, void * stream)
+{
+    return enc256v32_common(d_in, nblocks, d_starts, start0, true, d_out, out_cap, d_off, d_ws, ws_bytes, stream,
+                            "tpf_p4d1enc256v32_batch");
+}
+
+} // extern "C"

@@ -1,0 +1,258 @@
+// p4_block32.h -- wave-level decode of one 32-bit P4 block staged in LDS.
+//
+// Restates, for the GPU, the per-block decoders of the reference:
+//   p4Dec256v32   src/scalar/p4dec256v32_scalar.cpp:90-137   (modes below)
+//   p4D1Dec256v32 src/scalar/p4d1dec256v32_scalar.cpp:198-268
+//   p4Dec128v32   src/scalar/p4dec128v32_scalar.cpp          (L = 4 lanes)
+// Header byte h: (h&0xC0)==0xC0 constant; (h&0x40)==0 plain / bitmap patch
+// (h&0x80 plus bx byte); else vbyte exceptions (xn byte).
+//
+// Work split inside the wave: lane t owns the four consecutive values
+// 4t..4t+3 of a 256-value block, i.e. lanes 4(t&1)..4(t&1)+3 of interleave
+// group g = t>>1.  The four values share one lane-bit offset g*b, so the lane
+// reads the 16-byte word group k = g*b/32 and k+1 (5 aligned dwords each,
+// realigned with v_alignbyte) and funnel-shifts with v_alignbit.
+#pragma once
+
+#include "tpf_device.h"
+
+namespace tpf::dev
+{
+
+// Scratch per wave: 256 u32 exception values by position + 256 u32 temp.
+constexpr uint32_t kWaveScratchU32 = 512;
+
+// Unpack 4 values of lane t from the 256v32 (L=8) base layout at byte p.
+__device__ __forceinline__ u32x4 unpack256v32_lane(const uint32_t * lds, uint32_t p, uint32_t b, uint32_t t)
+{
+    const uint32_t g = t >> 1;
+    const uint32_t o = g * b;
+    const uint32_t pos = p + 32u * (o >> 5) + 16u * (t & 1u);
+    const uint32_t sh = o & 31u;
+    const uint32_t m = p & 3u;
+    const uint32_t q = pos >> 2;
+    const uint32_t d0 = lds[q], d1 = lds[q + 1], d2 = lds[q + 2], d3 = lds[q + 3], d4 = lds[q + 4];
+    const uint32_t e0 = lds[q + 8], e1 = lds[q + 9], e2 = lds[q + 10], e3 = lds[q + 11], e4 = lds[q + 12];
+    const uint32_t msk = mask32(b);
+    u32x4 v;
+    v.x = __builtin_amdgcn_alignbit(__builtin_amdgcn_alignbyte(e1, e0, m), __builtin_amdgcn_alignbyte(d1, d0, m), sh) & msk;
+    v.y = __builtin_amdgcn_alignbit(__builtin_amdgcn_alignbyte(e2, e1, m), __builtin_amdgcn_alignbyte(d2, d1, m), sh) & msk;
+    v.z = __builtin_amdgcn_alignbit(__builtin_amdgcn_alignbyte(e3, e2, m), __builtin_amdgcn_alignbyte(d3, d2, m), sh) & msk;
+    v.w = __builtin_amdgcn_alignbit(__builtin_amdgcn_alignbyte(e4, e3, m), __builtin_amdgcn_alignbyte(d4, d3, m), sh) & msk;
+    return v;
+}
+
+__device__ __forceinline__ uint32_t comp(const u32x4 & v, uint32_t j)
+{
+    return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
+}
+
+__device__ __forceinline__ void or_comp(u32x4 & v, uint32_t j, uint32_t x)
+{
+    if (j == 0)
+        v.x |= x;
+    else if (j == 1)
+        v.y |= x;
+    else if (j == 2)
+        v.z |= x;
+    else
+        v.w |= x;
+}
+
+// Bitmap-patch exceptions (p4Dec256PayloadBitmap, p4dec256v32_scalar.cpp:10-66):
+// 32-byte bitmap at bm_pos, then the xn exception high parts as ONE horizontal
+// LSB-first bx-bit stream (bitunpack32Scalar), then the base payload.  Lane t
+// ranks its own bitmap bits with popcounts instead of the serial ctz loop.
+// Returns the payload byte position; *xn_out = exception count.
+struct BitmapInfo
+{
+    uint32_t pc0, pc1, pc2, pc3;
+    uint64_t word; // bitmap word holding this lane's 4 bits
+};
+
+__device__ __forceinline__ BitmapInfo read_bitmap256(const uint32_t * lds, uint32_t bm_pos, uint32_t t)
+{
+    BitmapInfo bi;
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        w[i] = lds_u32(lds, bm_pos + 4u * i);
+    uint64_t b0 = (uint64_t(w[1]) << 32) | w[0];
+    uint64_t b1 = (uint64_t(w[3]) << 32) | w[2];
+    uint64_t b2 = (uint64_t(w[5]) << 32) | w[4];
+    uint64_t b3 = (uint64_t(w[7]) << 32) | w[6];
+    bi.pc0 = __builtin_popcountll(b0);
+    bi.pc1 = __builtin_popcountll(b1);
+    bi.pc2 = __builtin_popcountll(b2);
+    bi.pc3 = __builtin_popcountll(b3);
+    const uint32_t u = t >> 4;
+    bi.word = u == 0 ? b0 : u == 1 ? b1 : u == 2 ? b2 : b3;
+    return bi;
+}
+
+__device__ __forceinline__ void patch_bitmap256(const uint32_t * lds, const BitmapInfo & bi, uint32_t xs, uint32_t bx,
+                                                uint32_t b, uint32_t t, u32x4 & v)
+{
+    const uint32_t u = t >> 4;
+    const uint32_t bo = 4u * (t & 15u);
+    uint32_t before = (u > 0 ? bi.pc0 : 0u) + (u > 1 ? bi.pc1 : 0u) + (u > 2 ? bi.pc2 : 0u);
+    before += __builtin_popcountll(bi.word & ((1ull << bo) - 1ull));
+    const uint32_t my = static_cast<uint32_t>(bi.word >> bo) & 0xFu;
+    if (my == 0u)
+        return;
+    const uint32_t xsbit = xs * 8u;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j)
+    {
+        if ((my >> j) & 1u)
+        {
+            const uint32_t k = before + __builtin_popcount(my & ((1u << j) - 1u));
+            const uint32_t e = lds_bits(lds, xsbit + k * bx, bx);
+            or_comp(v, j, shl32(e, b));
+        }
+    }
+}
+
+// vbyte exceptions (p4dec256v32_scalar.cpp:123-136; vbDec32 p4_scalar_internal.cpp:215-237,
+// vbGet32Inline p4_scalar_internal.h:589-625).  V starts at v0: either
+// 0xFF + 4*xn raw LE words, or xn vbytes whose lengths are decided by their
+// marker byte.  The compressed stream is split in 64-byte windows: each lane
+// classifies one byte, ballots give 64-bit length masks and a wave-uniform
+// (SALU) chain walk finds the value starts; each start lane decodes its value.
+// Exception values are OR-ed into scr[pos] (ds_or, so duplicate positions
+// behave like the reference's sequential |=).  Returns the byte position just
+// past the position list.
+__device__ __forceinline__ uint32_t vbyte_exceptions(const uint32_t * lds, uint32_t v0, uint32_t xn, uint32_t * scr,
+                                                     uint32_t t)
+{
+    uint32_t * tmp = scr + 256;
+    reinterpret_cast<u32x4 *>(scr)[t] = u32x4{0u, 0u, 0u, 0u};
+    wave_lds_sync();
+    const uint32_t first = uni(lds_byte(lds, v0));
+    uint32_t vend;
+    if (first == 0xFFu)
+    {
+        const uint32_t pbase = v0 + 1u + 4u * xn;
+        for (uint32_t k = t; k < xn; k += kWave)
+        {
+            const uint32_t val = lds_u32(lds, v0 + 1u + 4u * k);
+            const uint32_t pos = lds_byte(lds, pbase + k);
+            atomicOr(&scr[pos], val);
+        }
+        vend = pbase;
+    }
+    else
+    {
+        uint32_t c = v0, sp = 0, found = 0;
+        vend = v0;
+        while (found < xn)
+        {
+            const uint32_t by = lds_byte(lds, c + t);
+            const uint32_t len = by < 0x9Cu ? 1u : by < 0xDCu ? 2u : by < 0xFCu ? 3u : by == 0xFCu ? 4u : 5u;
+            const uint64_t L2 = __ballot(len >= 2u), L3 = __ballot(len >= 3u), L4 = __ballot(len >= 4u),
+                           L5 = __ballot(len >= 5u);
+            const uint32_t need = xn - found;
+            uint64_t M = 0;
+            uint32_t cnt = 0;
+            while (sp < 64u && cnt < need)
+            {
+                M |= 1ull << sp;
+                ++cnt;
+                sp += 1u + static_cast<uint32_t>((L2 >> sp) & 1ull) + static_cast<uint32_t>((L3 >> sp) & 1ull)
+                    + static_cast<uint32_t>((L4 >> sp) & 1ull) + static_cast<uint32_t>((L5 >> sp) & 1ull);
+            }
+            if ((M >> t) & 1ull)
+            {
+                const uint32_t k = found + __builtin_popcountll(M & lanemask_lt());
+                const uint32_t d = lds_u32(lds, c + t + 1u);
+                uint32_t val;
+                if (by < 0x9Cu)
+                    val = by;
+                else if (by < 0xDCu)
+                    val = ((by - 0x9Cu) << 8) + (d & 0xFFu) + 156u;
+                else if (by < 0xFCu)
+                    val = (d & 0xFFFFu) + ((by - 0xDCu) << 16) + 16540u;
+                else if (by == 0xFCu)
+                    val = d & 0xFFFFFFu;
+                else
+                    val = d;
+                tmp[k & 255u] = val;
+            }
+            found += cnt;
+            vend = c + sp;
+            if (sp >= 64u)
+            {
+                sp -= 64u;
+                c += 64u;
+            }
+        }
+        wave_lds_sync();
+        for (uint32_t k = t; k < xn; k += kWave)
+        {
+            const uint32_t pos = lds_byte(lds, vend + k);
+            atomicOr(&scr[pos], tmp[k]);
+        }
+    }
+    wave_lds_sync();
+    return vend + xn;
+}
+
+// Decode one 256v32 block at LDS byte s.  Returns consumed bytes (uniform).
+__device__ __forceinline__ uint32_t decode_block256v32(const uint32_t * lds, uint32_t s, uint32_t * scr, uint32_t t, u32x4 & v)
+{
+    const uint32_t h = uni(lds_byte(lds, s));
+    if ((h & 0xC0u) == 0xC0u)
+    {
+        const uint32_t b = h & 0x3Fu;
+        uint32_t c = lds_u32(lds, s + 1u);
+        if (b < 32u)
+            c &= mask32(b);
+        v = u32x4{c, c, c, c};
+        return 1u + ((b + 7u) >> 3);
+    }
+    if ((h & 0x40u) == 0u)
+    {
+        const uint32_t hdr = (h & 0x80u) ? 2u : 1u;
+        const uint32_t bx = (h & 0x80u) ? min(uni(lds_byte(lds, s + 1u)), 32u) : 0u;
+        const uint32_t b = min(h & 0x7Fu, 32u);
+        if (bx == 0u)
+        {
+            v = unpack256v32_lane(lds, s + hdr, b, t);
+            return hdr + 32u * b;
+        }
+        const BitmapInfo bi = read_bitmap256(lds, s + 2u, t);
+        const uint32_t xn = bi.pc0 + bi.pc1 + bi.pc2 + bi.pc3;
+        const uint32_t xs = s + 34u;
+        const uint32_t xbytes = (xn * bx + 7u) >> 3;
+        v = unpack256v32_lane(lds, xs + xbytes, b, t);
+        patch_bitmap256(lds, bi, xs, bx, b, t, v);
+        return 34u + xbytes + 32u * b;
+    }
+    const uint32_t b = min(h & 0x3Fu, 32u);
+    const uint32_t xn = uni(lds_byte(lds, s + 1u));
+    v = unpack256v32_lane(lds, s + 2u, b, t);
+    const uint32_t end = vbyte_exceptions(lds, s + 2u + 32u * b, xn, scr, t);
+    const u32x4 ex = reinterpret_cast<const u32x4 *>(scr)[t];
+    v.x |= shl32(ex.x, b);
+    v.y |= shl32(ex.y, b);
+    v.z |= shl32(ex.z, b);
+    v.w |= shl32(ex.w, b);
+    return end - s;
+}
+
+// Delta-1 (applyDelta1_256, p4d1dec256v32_scalar.cpp:39-50): inclusive scan
+// of v[i]+1 seeded with start, mod 2^32.  Per lane serial over its 4 values,
+// wave scan (DPP) over the 64 lane totals.  Returns the block's last value.
+__device__ __forceinline__ uint32_t apply_delta1_256(u32x4 & v, uint32_t start)
+{
+    const uint32_t a0 = v.x + 1u;
+    const uint32_t a1 = a0 + v.y + 1u;
+    const uint32_t a2 = a1 + v.z + 1u;
+    const uint32_t a3 = a2 + v.w + 1u;
+    const uint32_t incl = wave_incl_scan(a3);
+    const uint32_t base = start + incl - a3;
+    v = u32x4{base + a0, base + a1, base + a2, base + a3};
+    return start + __builtin_amdgcn_readlane(incl, 63);
+}
+
+} // namespace tpf::dev

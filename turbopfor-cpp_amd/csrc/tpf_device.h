@@ -1,0 +1,137 @@
+// tpf_device.h -- CDNA4 (gfx950) device helpers shared by the P4 kernels.
+//
+// All kernels decode/encode ONE P4 block per wave64.  Packed bytes are staged
+// into LDS with coalesced 16-byte buffer loads and read back with aligned
+// ds_read_b32 + v_alignbyte/v_alignbit funnel shifts, so no kernel ever issues
+// an unaligned memory access although P4 blocks start at arbitrary bytes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tpf::dev
+{
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr uint32_t kWave = 64;
+
+__device__ __forceinline__ uint32_t lane_id()
+{
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+// Broadcast lane 0's value: tells the compiler the value is wave-uniform so
+// the mode dispatch becomes scalar branches.
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+__device__ __forceinline__ uint64_t uni64(uint64_t x)
+{
+    uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x));
+    uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x >> 32));
+    return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t mask32(uint32_t b) { return b >= 32u ? 0xFFFFFFFFu : ((1u << b) - 1u); }
+
+__device__ __forceinline__ uint32_t shl32(uint32_t v, uint32_t b) { return b >= 32u ? 0u : (v << b); }
+
+// Order LDS traffic between lanes of ONE wave (a wave's DS ops execute in
+// order; this only stops the compiler from moving them across the point).
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---- LDS byte-stream readers (pos = byte offset into the dword array) -----
+__device__ __forceinline__ uint32_t lds_byte(const uint32_t * w, uint32_t pos)
+{
+    return reinterpret_cast<const uint8_t *>(w)[pos];
+}
+
+// 32 bits starting at byte pos (any alignment).
+__device__ __forceinline__ uint32_t lds_u32(const uint32_t * w, uint32_t pos)
+{
+    uint32_t q = pos >> 2;
+    return __builtin_amdgcn_alignbyte(w[q + 1], w[q], pos & 3u);
+}
+
+// nb (<= 32) bits starting at absolute bit position bp.
+__device__ __forceinline__ uint32_t lds_bits(const uint32_t * w, uint32_t bp, uint32_t nb)
+{
+    uint32_t q = bp >> 5;
+    return __builtin_amdgcn_alignbit(w[q + 1], w[q], bp & 31u) & mask32(nb);
+}
+
+// ---- wave64 inclusive scan (DPP row_shr + row_bcast, gfx9 idiom) ----------
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
+{
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false); // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false); // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false); // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false); // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false); // row_bcast:15
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false); // row_bcast:31
+    return x;
+}
+
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t x)
+{
+    // 64-bit scan from two 32-bit passes is not associative-safe; use shuffles.
+    for (uint32_t d = 1; d < 64; d <<= 1)
+    {
+        uint64_t y = __shfl_up(x, d, 64);
+        if (lane_id() >= d)
+            x += y;
+    }
+    return x;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x)
+{
+    uint32_t s = wave_incl_scan(x);
+    return __builtin_amdgcn_readlane(s, 63);
+}
+
+__device__ __forceinline__ uint32_t wave_or(uint32_t x)
+{
+    for (uint32_t d = 1; d < 64; d <<= 1)
+        x |= __shfl_xor(x, d, 64);
+    return x;
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt()
+{
+    uint32_t t = lane_id();
+    return t == 0 ? 0ull : (~0ull >> (64u - t));
+}
+
+// ---- buffer loads: OOB lanes read zeros (no fault, no slack required) -----
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void * base, uint32_t nbytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), static_cast<short>(0), static_cast<int>(nbytes),
+                                             0x00020000);
+}
+
+__device__ __forceinline__ u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    return __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), 0, 0);
+}
+
+// 16 bytes at base+off where only [0, avail) of base is readable.  Raw buffer
+// loads range-check the whole 16-byte access (a straddling load returns
+// zeros), so the single chunk that straddles the end is read byte by byte.
+__device__ __forceinline__ u32x4 load16_guarded(const uint8_t * base, __amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t avail)
+{
+    if (off + 16u <= avail)
+        return buf_load16(r, off);
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t i = 0; i < 16u; ++i)
+        if (off + i < avail)
+            w[i >> 2] |= static_cast<uint32_t>(base[off + i]) << (8u * (i & 3u));
+    return u32x4{w[0], w[1], w[2], w[3]};
+}
+
+} // namespace tpf::dev

@@ -1,0 +1,23 @@
+// tpf_kernels.h -- host-side launch functions of the HIP kernels (internal).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+namespace tpf
+{
+
+// Workgroups to launch for a grid-stride kernel: per_cu workgroups on every
+// CU of the current device (cached per device).
+uint64_t grid_cap(hipStream_t stream, uint32_t per_cu);
+
+hipError_t launch_dec256v32(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * out,
+                            const uint32_t * starts, unsigned long long * err, hipStream_t stream);
+
+size_t enc256v32_workspace(uint64_t nblocks);
+hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, bool d1,
+                            uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t stream);
+
+} // namespace tpf

@@ -1,0 +1,116 @@
+"""Python host binding of libturbopfor_amd.so (ctypes over the C-ABI in
+include/turbopfor_gpu.h).  Device buffers are torch tensors on a HIP device;
+kernels run on torch's current stream.  There is no CPU fallback: every
+entry point raises if the HIP library or device is missing.
+
+Reference interface mirrored: include/turbopfor.h of amosbird/TurboPFor-CPP
+(per-block p4Enc*/p4Dec*), lifted to batches of blocks with explicit byte
+offsets (the reference's callers chain blocks through the returned pointer).
+"""
+import ctypes
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libturbopfor_amd.so")
+
+_lib = None
+
+c_u64 = ctypes.c_uint64
+c_vp = ctypes.c_void_p
+
+
+class TpfError(RuntimeError):
+    pass
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", PKG_DIR, f"-j{min(os.cpu_count() or 4, 16)}"])
+
+
+def lib():
+    """Load (building if needed) the in-tree HIP library."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        L.tpf_last_error.restype = ctypes.c_char_p
+        L.tpf_device_count.restype = ctypes.c_int
+        L.tpf_p4dec256v32_batch.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp, c_vp]
+        L.tpf_p4d1dec256v32_batch.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp, c_vp, c_vp]
+        L.tpf_p4enc256v32_bound.argtypes = [c_u64]
+        L.tpf_p4enc256v32_bound.restype = c_u64
+        L.tpf_p4enc256v32_workspace_size.argtypes = [c_u64]
+        L.tpf_p4enc256v32_workspace_size.restype = ctypes.c_size_t
+        L.tpf_p4enc256v32_batch.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp, ctypes.c_size_t, c_vp]
+        L.tpf_p4d1enc256v32_batch.argtypes = [c_vp, c_u64, c_vp, ctypes.c_uint32, c_vp, c_u64, c_vp, c_vp,
+                                              ctypes.c_size_t, c_vp]
+        for name in ("tpf_p4dec256v32_batch", "tpf_p4d1dec256v32_batch", "tpf_p4enc256v32_batch",
+                     "tpf_p4d1enc256v32_batch"):
+            getattr(L, name).restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise TpfError(f"turbopfor_amd error {rc}: {lib().tpf_last_error().decode()}")
+
+
+def _stream(torch):
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def dec256v32(packed, offsets, nblocks, out=None, starts=None, err=None):
+    """Decode nblocks 256v32 blocks.  packed: uint8 CUDA tensor; offsets:
+    int64 CUDA tensor [nblocks+1]; starts: optional int32 [nblocks] for the
+    delta-1 variant (p4D1Dec256v32).  Returns int32 tensor [nblocks, 256]
+    (bit pattern = uint32)."""
+    import torch
+
+    if out is None:
+        out = torch.empty((nblocks, 256), dtype=torch.int32, device=packed.device)
+    L = lib()
+    if starts is None:
+        rc = L.tpf_p4dec256v32_batch(_ptr(packed), packed.numel(), _ptr(offsets), nblocks, _ptr(out), _ptr(err),
+                                     _stream(torch))
+    else:
+        rc = L.tpf_p4d1dec256v32_batch(_ptr(packed), packed.numel(), _ptr(offsets), nblocks, _ptr(out),
+                                       _ptr(starts), _ptr(err), _stream(torch))
+    _check(rc)
+    return out
+
+
+def enc256v32(values, d1=False, starts=None, start0=0, out=None):
+    """Encode values (int32/uint32-bit CUDA tensor, nblocks*256 elements) as
+    256v32 P4 blocks.  Returns (packed uint8 tensor sized to the encoded
+    total, offsets int64 tensor [nblocks+1]).  d1 selects p4D1Enc256v32:
+    starts (int32 [nblocks]) gives each block's preceding value, or with
+    starts=None the blocks form one chained list starting after start0."""
+    import torch
+
+    assert values.is_cuda and values.dtype in (torch.int32,) and values.numel() % 256 == 0
+    values = values.contiguous()
+    nb = values.numel() // 256
+    L = lib()
+    cap = int(L.tpf_p4enc256v32_bound(nb))
+    if out is None:
+        out = torch.empty(cap, dtype=torch.uint8, device=values.device)
+    offs = torch.empty(nb + 1, dtype=torch.int64, device=values.device)
+    ws_bytes = int(L.tpf_p4enc256v32_workspace_size(nb))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=values.device)
+    if d1:
+        rc = L.tpf_p4d1enc256v32_batch(_ptr(values), nb, _ptr(starts), ctypes.c_uint32(start0 & 0xFFFFFFFF),
+                                       _ptr(out), out.numel(), _ptr(offs), _ptr(ws), ws_bytes, _stream(torch))
+    else:
+        rc = L.tpf_p4enc256v32_batch(_ptr(values), nb, _ptr(out), out.numel(), _ptr(offs), _ptr(ws), ws_bytes,
+                                     _stream(torch))
+    _check(rc)
+    total = int(offs[-1].item())
+    return out[:total], offs
