@@ -33,6 +33,11 @@ def lib():
     """Load (building if needed) the in-tree HIP library."""
     global _lib
     if _lib is None:
+        # torch bundles its own libamdhip64 (soname libamdhip64.so.7, file
+        # name libamdhip64.so).  Load it first so our library binds to that
+        # same HIP runtime instead of a second copy from /opt/rocm.
+        import torch  # noqa: F401
+
         if not os.path.exists(LIB_PATH):
             build()
         L = ctypes.CDLL(LIB_PATH)
