@@ -32,6 +32,10 @@ __device__ __forceinline__ uint64_t uni64(uint64_t x)
     return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
+// Integer min (HIP's min<uint64_t> can resolve to a double overload).
+__device__ __forceinline__ uint64_t min_u64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint64_t sub_sat(uint64_t a, uint64_t b) { return a > b ? a - b : 0u; }
+
 __device__ __forceinline__ uint32_t mask32(uint32_t b) { return b >= 32u ? 0xFFFFFFFFu : ((1u << b) - 1u); }
 
 __device__ __forceinline__ uint32_t shl32(uint32_t v, uint32_t b) { return b >= 32u ? 0u : (v << b); }
@@ -109,10 +113,14 @@ __device__ __forceinline__ uint64_t lanemask_lt()
 }
 
 // ---- buffer loads: OOB lanes read zeros (no fault, no slack required) -----
+// Descriptor inputs are forced through readfirstlane so the compiler can
+// prove the SRD wave-uniform (otherwise every buffer op is wrapped in a
+// readfirstlane "waterfall" loop, cdna_hip_programming.md T20).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void * base, uint32_t nbytes)
 {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), static_cast<short>(0), static_cast<int>(nbytes),
-                                             0x00020000);
+    const uint64_t b = uni64(reinterpret_cast<uint64_t>(base));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(b), static_cast<short>(0),
+                                             static_cast<int>(uni(nbytes)), 0x00020000);
 }
 
 __device__ __forceinline__ u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t off)
