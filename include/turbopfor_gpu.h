@@ -68,6 +68,34 @@ int tpf_p4enc256v32_batch(const uint32_t *d_in, uint64_t nblocks, uint8_t *d_out
 int tpf_p4d1enc256v32_batch(const uint32_t *d_in, uint64_t nblocks, const uint32_t *d_starts, uint32_t start0,
                             uint8_t *d_out, uint64_t out_cap, uint64_t *d_off, void *d_ws, size_t ws_bytes, void *stream);
 
+/* ---- every format of include/turbopfor.h, batched ----------------------
+ * fmt selects the reference function family:
+ *   TPF_FMT_32     p4{,D1}{Enc,Dec}32      (turbopfor.h:9-18)   n = 1..256 values per block
+ *   TPF_FMT_128V32 p4{,D1}{Enc,Dec}128v32  (turbopfor.h:21-30)  n <= 128
+ *   TPF_FMT_256V32 p4{,D1}{Enc,Dec}256v32  (turbopfor.h:33-42)  n <= 256 (n == 256 -> hot path)
+ *   TPF_FMT_64     p4{,D1}{Enc,Dec}64      (turbopfor.h:45-54)  n = 1..256 (uint64)
+ *   TPF_FMT_128V64 p4{,D1}{Enc,Dec}128v64  (turbopfor.h:57-67)  n == 128 (uint64)
+ *   TPF_FMT_256V64 p4{,D1}{Enc,Dec}256v64  (turbopfor.h:69-80)  n == 256 (uint64; one unit = two 128v64 blocks)
+ * A batch holds nblocks units; unit i's values are at d_vals + i*stride with
+ * stride = n for the horizontal formats and the layout's full width (128 or
+ * 256) for the interleaved ones (the reference packs the full width).
+ * Values are uint32 or uint64 as the family requires.  D1 (delta-1): starts
+ * per unit, or NULL = one chained list (encode: start0 then the previous
+ * unit's last input; decode requires starts). */
+#define TPF_FMT_32 0
+#define TPF_FMT_128V32 1
+#define TPF_FMT_256V32 2
+#define TPF_FMT_64 3
+#define TPF_FMT_128V64 4
+#define TPF_FMT_256V64 5
+
+uint64_t tpf_enc_bound(int fmt, uint64_t nblocks, unsigned n);
+size_t tpf_enc_workspace_size(int fmt, uint64_t nblocks, unsigned n);
+int tpf_dec_batch(int fmt, const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks, unsigned n,
+                  void *d_vals, const void *d_starts, uint64_t *d_err, void *stream);
+int tpf_enc_batch(int fmt, const void *d_vals, uint64_t nblocks, unsigned n, int d1, const void *d_starts, uint64_t start0,
+                  uint8_t *d_out, uint64_t out_cap, uint64_t *d_off, void *d_ws, size_t ws_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -139,4 +139,95 @@ int tpf_p4d1enc256v32_batch(const uint32_t * d_in, uint64_t nblocks, const uint3
                             "tpf_p4d1enc256v32_batch");
 }
 
+static bool fmt_ok(int fmt, unsigned n)
+{
+    switch (fmt)
+    {
+        case TPF_FMT_32:
+        case TPF_FMT_64:
+            return n >= 1 && n <= 256;
+        case TPF_FMT_128V32:
+            return n >= 1 && n <= 128;
+        case TPF_FMT_256V32:
+            return n >= 1 && n <= 256;
+        case TPF_FMT_128V64:
+            return n == 128;
+        case TPF_FMT_256V64:
+            return n == 256;
+        default:
+            return false;
+    }
+}
+
+static unsigned unit_values(int fmt, unsigned n)
+{
+    switch (fmt)
+    {
+        case TPF_FMT_128V32:
+        case TPF_FMT_128V64:
+            return 128;
+        case TPF_FMT_256V32:
+        case TPF_FMT_256V64:
+            return 256;
+        default:
+            return n;
+    }
+}
+
+uint64_t tpf_enc_bound(int fmt, uint64_t nblocks, unsigned n)
+{
+    const bool wide = fmt == TPF_FMT_64 || fmt == TPF_FMT_128V64 || fmt == TPF_FMT_256V64;
+    return nblocks * (64u + (wide ? 18u : 8u) * unit_values(fmt, n)) + 64u;
+}
+
+size_t tpf_enc_workspace_size(int fmt, uint64_t nblocks, unsigned n)
+{
+    if (fmt == TPF_FMT_256V32 && n == 256)
+        return tpf::enc256v32_workspace(nblocks);
+    return tpf::generic_workspace(nblocks);
+}
+
+int tpf_dec_batch(int fmt, const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nblocks, unsigned n, void * d_vals,
+                  const void * d_starts, uint64_t * d_err, void * stream)
+{
+    if (int rc = check_device())
+        return rc;
+    if (!fmt_ok(fmt, n))
+        return fail(TPF_EINVAL, "tpf_dec_batch: unsupported (fmt, n)");
+    if (nblocks && (!d_in || !d_off || !d_vals))
+        return fail(TPF_EINVAL, "tpf_dec_batch: null pointer");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (int rc = prep_err(d_err, s))
+        return rc;
+    hipError_t e;
+    if (fmt == TPF_FMT_256V32 && n == 256)
+        e = tpf::launch_dec256v32(d_in, in_bytes, d_off, nblocks, static_cast<uint32_t *>(d_vals),
+                                  static_cast<const uint32_t *>(d_starts), reinterpret_cast<unsigned long long *>(d_err), s);
+    else
+        e = tpf::launch_dec_generic(fmt, d_in, in_bytes, d_off, nblocks, n, d_vals, d_starts,
+                                    reinterpret_cast<unsigned long long *>(d_err), s);
+    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_dec_batch");
+}
+
+int tpf_enc_batch(int fmt, const void * d_vals, uint64_t nblocks, unsigned n, int d1, const void * d_starts, uint64_t start0,
+                  uint8_t * d_out, uint64_t out_cap, uint64_t * d_off, void * d_ws, size_t ws_bytes, void * stream)
+{
+    if (int rc = check_device())
+        return rc;
+    if (!fmt_ok(fmt, n))
+        return fail(TPF_EINVAL, "tpf_enc_batch: unsupported (fmt, n)");
+    if (!d_off || (nblocks && (!d_vals || !d_out || !d_ws)))
+        return fail(TPF_EINVAL, "tpf_enc_batch: null pointer");
+    if (ws_bytes < tpf_enc_workspace_size(fmt, nblocks, n))
+        return fail(TPF_EINVAL, "tpf_enc_batch: workspace too small");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e;
+    if (fmt == TPF_FMT_256V32 && n == 256)
+        e = tpf::launch_enc256v32(static_cast<const uint32_t *>(d_vals), nblocks, static_cast<const uint32_t *>(d_starts),
+                                  static_cast<uint32_t>(start0), d1 != 0, d_out, out_cap, d_off, d_ws, ws_bytes, s);
+    else
+        e = tpf::launch_enc_generic(fmt, d_vals, nblocks, n, d1 != 0, d_starts, start0, d_out, out_cap, d_off, d_ws, ws_bytes, s);
+    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_enc_batch");
+}
+
 } // extern "C"

@@ -36,6 +36,15 @@ __device__ __forceinline__ uint64_t uni64(uint64_t x)
 __device__ __forceinline__ uint64_t min_u64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint64_t sub_sat(uint64_t a, uint64_t b) { return a > b ? a - b : 0u; }
 
+// v_readlane of a 64-bit value.  (__builtin_amdgcn_readlane returns int: OR-ing
+// it into a uint64_t directly would sign-extend the low word.)
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t x, uint32_t l)
+{
+    const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(x)), l));
+    const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(x >> 32)), l));
+    return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
 __device__ __forceinline__ uint32_t mask32(uint32_t b) { return b >= 32u ? 0xFFFFFFFFu : ((1u << b) - 1u); }
 
 __device__ __forceinline__ uint32_t shl32(uint32_t v, uint32_t b) { return b >= 32u ? 0u : (v << b); }

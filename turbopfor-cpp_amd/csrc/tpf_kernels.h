@@ -13,6 +13,23 @@ namespace tpf
 // CU of the current device (cached per device).
 uint64_t grid_cap(hipStream_t stream, uint32_t per_cu);
 
+// format ids (== TPF_FMT_* of include/turbopfor_gpu.h)
+enum : int
+{
+    FMT_32 = 0,
+    FMT_128V32 = 1,
+    FMT_256V32 = 2,
+    FMT_64 = 3,
+    FMT_128V64 = 4,
+    FMT_256V64 = 5,
+};
+
+size_t generic_workspace(uint64_t nblocks);
+hipError_t launch_dec_generic(int fmt, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t n,
+                              void * out, const void * starts, unsigned long long * err, hipStream_t s);
+hipError_t launch_enc_generic(int fmt, const void * in, uint64_t nblocks, uint32_t n, bool d1, const void * starts, uint64_t start0,
+                              uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t s);
+
 hipError_t launch_dec256v32(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * out,
                             const uint32_t * starts, unsigned long long * err, hipStream_t stream);
 

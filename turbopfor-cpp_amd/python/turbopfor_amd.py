@@ -52,8 +52,15 @@ def lib():
         L.tpf_p4enc256v32_batch.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp, ctypes.c_size_t, c_vp]
         L.tpf_p4d1enc256v32_batch.argtypes = [c_vp, c_u64, c_vp, ctypes.c_uint32, c_vp, c_u64, c_vp, c_vp,
                                               ctypes.c_size_t, c_vp]
+        L.tpf_enc_bound.argtypes = [ctypes.c_int, c_u64, ctypes.c_uint]
+        L.tpf_enc_bound.restype = c_u64
+        L.tpf_enc_workspace_size.argtypes = [ctypes.c_int, c_u64, ctypes.c_uint]
+        L.tpf_enc_workspace_size.restype = ctypes.c_size_t
+        L.tpf_dec_batch.argtypes = [ctypes.c_int, c_vp, c_u64, c_vp, c_u64, ctypes.c_uint, c_vp, c_vp, c_vp, c_vp]
+        L.tpf_enc_batch.argtypes = [ctypes.c_int, c_vp, c_u64, ctypes.c_uint, ctypes.c_int, c_vp, c_u64, c_vp, c_u64,
+                                    c_vp, c_vp, ctypes.c_size_t, c_vp]
         for name in ("tpf_p4dec256v32_batch", "tpf_p4d1dec256v32_batch", "tpf_p4enc256v32_batch",
-                     "tpf_p4d1enc256v32_batch"):
+                     "tpf_p4d1enc256v32_batch", "tpf_dec_batch", "tpf_enc_batch"):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -119,3 +126,47 @@ def enc256v32(values, d1=False, starts=None, start0=0, out=None):
     _check(rc)
     total = int(offs[-1].item())
     return out[:total], offs
+
+
+# ---- every turbopfor.h family (include/turbopfor_gpu.h tpf_{enc,dec}_batch) ----
+FMT = {"32": 0, "128v32": 1, "256v32": 2, "64": 3, "128v64": 4, "256v64": 5}
+_WIDE = {"64", "128v64", "256v64"}
+_UNIT = {"128v32": 128, "256v32": 256, "128v64": 128, "256v64": 256}
+
+
+def unit_values(fmt, n):
+    return _UNIT.get(fmt, n)
+
+
+def enc_batch(fmt, values, nblocks, n, d1=False, starts=None, start0=0):
+    """values: int32/int64 CUDA tensor with nblocks*unit_values(fmt, n)
+    elements (bit patterns of uint32/uint64).  Returns (packed, offsets)."""
+    import torch
+
+    values = values.contiguous()
+    assert values.numel() == nblocks * unit_values(fmt, n)
+    L = lib()
+    f = FMT[fmt]
+    cap = int(L.tpf_enc_bound(f, nblocks, n))
+    out = torch.empty(cap, dtype=torch.uint8, device=values.device)
+    offs = torch.empty(nblocks + 1, dtype=torch.int64, device=values.device)
+    wsb = int(L.tpf_enc_workspace_size(f, nblocks, n))
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=values.device)
+    rc = L.tpf_enc_batch(f, _ptr(values), nblocks, n, 1 if d1 else 0, _ptr(starts),
+                         ctypes.c_uint64(start0 & ((1 << 64) - 1)), _ptr(out), cap, _ptr(offs), _ptr(ws), wsb,
+                         _stream(torch))
+    _check(rc)
+    return out[: int(offs[-1].item())], offs
+
+
+def dec_batch(fmt, packed, offsets, nblocks, n, starts=None, err=None, out=None):
+    import torch
+
+    dt = torch.int64 if fmt in _WIDE else torch.int32
+    if out is None:
+        out = torch.zeros(nblocks * unit_values(fmt, n), dtype=dt, device=packed.device)
+    L = lib()
+    rc = L.tpf_dec_batch(FMT[fmt], _ptr(packed), packed.numel(), _ptr(offsets), nblocks, n, _ptr(out), _ptr(starts),
+                         _ptr(err), _stream(torch))
+    _check(rc)
+    return out
