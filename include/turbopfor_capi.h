@@ -1,0 +1,81 @@
+/*
+ * turbopfor_capi.h -- extern "C" mirror of the reference's per-block API plus
+ * host-memory stream entry points.  This is the surface a foreign-language
+ * binding (cgo, JNI, N-API, ctypes) binds: plain C types, C linkage, one symbol
+ * per reference function.  See INTEGRATION.md.
+ *
+ * tpf_<name>(...) has exactly the argument meaning and return value of
+ * turbopfor::<name>(...) in the reference's include/turbopfor.h (line cited
+ * per family).  On failure (no HIP device, HIP error) these return NULL and
+ * tpf_last_error() describes why; they never fall back to a CPU codec.
+ */
+#ifndef TURBOPFOR_CAPI_H
+#define TURBOPFOR_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char *tpf_last_error(void);
+
+/* reference include/turbopfor.h:9-18 */
+unsigned char *tpf_p4Enc32(uint32_t *in, unsigned n, unsigned char *out);
+unsigned char *tpf_p4D1Enc32(uint32_t *in, unsigned n, unsigned char *out, uint32_t start);
+const unsigned char *tpf_p4Dec32(const unsigned char *in, unsigned n, uint32_t *out);
+const unsigned char *tpf_p4D1Dec32(const unsigned char *in, unsigned n, uint32_t *out, uint32_t start);
+/* :21-30 */
+unsigned char *tpf_p4Enc128v32(uint32_t *in, unsigned n, unsigned char *out);
+unsigned char *tpf_p4D1Enc128v32(uint32_t *in, unsigned n, unsigned char *out, uint32_t start);
+const unsigned char *tpf_p4Dec128v32(const unsigned char *in, unsigned n, uint32_t *out);
+const unsigned char *tpf_p4D1Dec128v32(const unsigned char *in, unsigned n, uint32_t *out, uint32_t start);
+/* :33-42 (hot path) */
+unsigned char *tpf_p4Enc256v32(uint32_t *in, unsigned n, unsigned char *out);
+unsigned char *tpf_p4D1Enc256v32(uint32_t *in, unsigned n, unsigned char *out, uint32_t start);
+const unsigned char *tpf_p4Dec256v32(const unsigned char *in, unsigned n, uint32_t *out);
+const unsigned char *tpf_p4D1Dec256v32(const unsigned char *in, unsigned n, uint32_t *out, uint32_t start);
+/* :45-54 */
+unsigned char *tpf_p4Enc64(uint64_t *in, unsigned n, unsigned char *out);
+unsigned char *tpf_p4D1Enc64(uint64_t *in, unsigned n, unsigned char *out, uint64_t start);
+const unsigned char *tpf_p4Dec64(const unsigned char *in, unsigned n, uint64_t *out);
+const unsigned char *tpf_p4D1Dec64(const unsigned char *in, unsigned n, uint64_t *out, uint64_t start);
+/* :57-67 */
+unsigned char *tpf_p4Enc128v64(uint64_t *in, unsigned n, unsigned char *out);
+unsigned char *tpf_p4D1Enc128v64(uint64_t *in, unsigned n, unsigned char *out, uint64_t start);
+const unsigned char *tpf_p4Dec128v64(const unsigned char *in, unsigned n, uint64_t *out);
+const unsigned char *tpf_p4D1Dec128v64(const unsigned char *in, unsigned n, uint64_t *out, uint64_t start);
+/* :69-80 */
+unsigned char *tpf_p4Enc256v64(uint64_t *in, unsigned n, unsigned char *out);
+unsigned char *tpf_p4D1Enc256v64(uint64_t *in, unsigned n, unsigned char *out, uint64_t start);
+const unsigned char *tpf_p4Dec256v64(const unsigned char *in, unsigned n, uint64_t *out);
+const unsigned char *tpf_p4D1Dec256v64(const unsigned char *in, unsigned n, uint64_t *out, uint64_t start);
+
+/* ---- stream framing (host, no decoding) -------------------
+ * Encoded length of the block at `in` (fmt = TPF_FMT_*, n = values per call),
+ * reading at most `avail` bytes; 0 if malformed/truncated.  values_written
+ * (optional) receives how many values the reference decoder stores (n for a
+ * constant block, else the layout's full width). */
+uint64_t tpf_block_size(int fmt, const uint8_t *in, uint64_t avail, unsigned n, int *values_written);
+/* Offsets of nblocks consecutive blocks (off[nblocks] = total).  Returns the
+ * total byte length, or -(i+1) if block i is malformed/truncated. */
+int64_t tpf_scan_offsets(int fmt, const uint8_t *in, uint64_t in_bytes, unsigned n, uint64_t nblocks, uint64_t *off);
+
+/* ---- host-memory streams (end-to-end path) ----------------
+ * Decode / encode nblocks blocks whose bytes and values live in HOST memory:
+ * the work is split into chunks that are copied to HBM, processed and copied
+ * back with H2D / kernel / D2H overlapped on separate HIP streams.  Host
+ * buffers allocated with hipHostMalloc (or registered) give full PCIe rate;
+ * pageable buffers are registered for the duration of the call.
+ * h_off may be NULL for decode (offsets are scanned with tpf_scan_offsets).
+ * Value arrays use the unit strides documented in turbopfor_gpu.h. */
+int tpf_host_dec(int fmt, const uint8_t *h_in, uint64_t in_bytes, const uint64_t *h_off, uint64_t nblocks, unsigned n,
+                 void *h_vals, const void *h_starts);
+int tpf_host_enc(int fmt, const void *h_vals, uint64_t nblocks, unsigned n, int d1, const void *h_starts, uint64_t start0,
+                 uint8_t *h_out, uint64_t out_cap, uint64_t *h_off);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -47,6 +47,8 @@ int prep_err(uint64_t * d_err, hipStream_t s)
 
 namespace tpf
 {
+void set_last_error(const std::string & msg) { g_err = msg; }
+
 uint64_t grid_cap(hipStream_t, uint32_t per_cu)
 {
     static int cus[64] = {0};

@@ -1,0 +1,379 @@
+// host_api.cpp -- the drop-in boundary: include/turbopfor.h (C++ linkage,
+// signature-identical to the reference's include/turbopfor.h:9-80), its
+// extern "C" mirror include/turbopfor_capi.h, and the host-memory stream
+// entry points.  Every call runs the gfx950 kernels through the batched
+// C-ABI (capi.cpp); nothing here encodes or decodes a value on the CPU.
+//
+// Per-block calls keep a thread-local context (HIP stream, device buffers,
+// pinned staging) on the thread's current device: copy one block's values or
+// bytes to HBM, launch with nblocks = 1, copy the result back, synchronise.
+// That is latency-bound (tens of microseconds per call) and exists so that a
+// reference caller relinks and gets identical bytes; throughput callers use
+// tpf_host_dec/tpf_host_enc (pipelined host streams) or turbopfor_gpu.h
+// (device-resident batches).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/turbopfor.h"
+#include "../../include/turbopfor_capi.h"
+#include "../../include/turbopfor_gpu.h"
+
+namespace
+{
+
+void hip_check(hipError_t e, const char * what)
+{
+    if (e != hipSuccess)
+        throw std::runtime_error(std::string("turbopfor_amd: ") + what + ": " + hipGetErrorString(e));
+}
+
+void tpf_check(int rc, const char * what)
+{
+    if (rc != TPF_OK)
+        throw std::runtime_error(std::string("turbopfor_amd: ") + what + ": " + tpf_last_error());
+}
+
+bool wide_fmt(int fmt) { return fmt == TPF_FMT_64 || fmt == TPF_FMT_128V64 || fmt == TPF_FMT_256V64; }
+
+unsigned unit_values(int fmt, unsigned n)
+{
+    switch (fmt)
+    {
+        case TPF_FMT_128V32:
+        case TPF_FMT_128V64:
+            return 128;
+        case TPF_FMT_256V32:
+        case TPF_FMT_256V64:
+            return 256;
+        default:
+            return n;
+    }
+}
+
+struct DevBuf
+{
+    void * p = nullptr;
+    size_t n = 0;
+    void release()
+    {
+        if (p)
+            (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    void * get(size_t want)
+    {
+        if (want > n)
+        {
+            if (p)
+                (void)hipFree(p);
+            p = nullptr;
+            hip_check(hipMalloc(&p, want), "hipMalloc");
+            n = want;
+        }
+        return p;
+    }
+    ~DevBuf()
+    {
+        if (p)
+            (void)hipFree(p);
+    }
+};
+
+struct HostBuf
+{
+    void * p = nullptr;
+    size_t n = 0;
+    void release()
+    {
+        if (p)
+            (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    void * get(size_t want)
+    {
+        if (want > n)
+        {
+            if (p)
+                (void)hipHostFree(p);
+            p = nullptr;
+            hip_check(hipHostMalloc(&p, want, hipHostMallocDefault), "hipHostMalloc");
+            n = want;
+        }
+        return p;
+    }
+    ~HostBuf()
+    {
+        if (p)
+            (void)hipHostFree(p);
+    }
+};
+
+// Thread-local per-block context.
+struct Ctx
+{
+    int device = -1;
+    hipStream_t stream = nullptr;
+    DevBuf d_in, d_vals, d_off, d_ws, d_start, d_err;
+    HostBuf h_in, h_vals, h_off;
+
+    static Ctx & get()
+    {
+        thread_local Ctx c;
+        int dev = 0;
+        int count = 0;
+        if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+            throw std::runtime_error("turbopfor_amd: no HIP device visible (this library has no CPU fallback)");
+        hip_check(hipGetDevice(&dev), "hipGetDevice");
+        if (c.device != dev)
+        {
+            c.reset();
+            c.device = dev;
+            hip_check(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking), "hipStreamCreate");
+        }
+        return c;
+    }
+    void reset()
+    {
+        for (DevBuf * b : {&d_in, &d_vals, &d_off, &d_ws, &d_start, &d_err})
+            b->release();
+        for (HostBuf * b : {&h_in, &h_vals, &h_off})
+            b->release();
+        if (stream)
+            (void)hipStreamDestroy(stream);
+        stream = nullptr;
+    }
+    ~Ctx() { reset(); }
+};
+
+// One-block encode through tpf_enc_batch.
+unsigned char * enc_one(int fmt, const void * in, unsigned n, unsigned char * out, bool d1, uint64_t start)
+{
+    if (n == 0)
+        return out;
+    Ctx & c = Ctx::get();
+    const size_t es = wide_fmt(fmt) ? 8 : 4;
+    const size_t vbytes = es * unit_values(fmt, n);
+    const uint64_t cap = tpf_enc_bound(fmt, 1, n);
+    void * hv = c.h_vals.get(vbytes);
+    std::memcpy(hv, in, vbytes); // the reference also reads the full block width
+    void * dv = c.d_vals.get(vbytes);
+    auto * dout = static_cast<uint8_t *>(c.d_in.get(cap));
+    auto * doff = static_cast<uint64_t *>(c.d_off.get(2 * sizeof(uint64_t)));
+    const size_t wsb = tpf_enc_workspace_size(fmt, 1, n);
+    void * ws = c.d_ws.get(std::max<size_t>(wsb, 256));
+    hip_check(hipMemcpyAsync(dv, hv, vbytes, hipMemcpyHostToDevice, c.stream), "H2D values");
+    tpf_check(tpf_enc_batch(fmt, dv, 1, n, d1 ? 1 : 0, nullptr, start, dout, cap, doff, ws, std::max<size_t>(wsb, 256), c.stream),
+              "tpf_enc_batch");
+    auto * hoff = static_cast<uint64_t *>(c.h_off.get(2 * sizeof(uint64_t)));
+    auto * hin = static_cast<uint8_t *>(c.h_in.get(cap));
+    hip_check(hipMemcpyAsync(hoff, doff, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream), "D2H offsets");
+    hip_check(hipMemcpyAsync(hin, dout, cap, hipMemcpyDeviceToHost, c.stream), "D2H bytes");
+    hip_check(hipStreamSynchronize(c.stream), "sync");
+    const uint64_t size = hoff[1];
+    std::memcpy(out, hin, size);
+    return out + size;
+}
+
+// One-block decode through tpf_dec_batch.
+const unsigned char * dec_one(int fmt, const unsigned char * in, unsigned n, void * out, bool d1, uint64_t start)
+{
+    if (n == 0)
+        return in;
+    Ctx & c = Ctx::get();
+    int written = 0;
+    // the block's length comes from its own header (framing.cpp); 1 MiB is far
+    // above any block's size and only bounds the header walk
+    const uint64_t size = tpf_block_size(fmt, in, uint64_t(1) << 20, n, &written);
+    if (size == 0)
+        throw std::runtime_error("turbopfor_amd: malformed P4 block header");
+    const size_t es = wide_fmt(fmt) ? 8 : 4;
+    const size_t vbytes = es * unit_values(fmt, n);
+    auto * hin = static_cast<uint8_t *>(c.h_in.get(size));
+    std::memcpy(hin, in, size);
+    auto * din = static_cast<uint8_t *>(c.d_in.get(size));
+    auto * doff = static_cast<uint64_t *>(c.d_off.get(2 * sizeof(uint64_t)));
+    auto * hoff = static_cast<uint64_t *>(c.h_off.get(4 * sizeof(uint64_t)));
+    hoff[0] = 0;
+    hoff[1] = size;
+    hoff[2] = start;
+    void * dv = c.d_vals.get(vbytes);
+    void * dstart = c.d_start.get(8);
+    hip_check(hipMemcpyAsync(din, hin, size, hipMemcpyHostToDevice, c.stream), "H2D bytes");
+    hip_check(hipMemcpyAsync(doff, hoff, 2 * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream), "H2D offsets");
+    if (d1)
+        hip_check(hipMemcpyAsync(dstart, &hoff[2], es, hipMemcpyHostToDevice, c.stream), "H2D start");
+    tpf_check(tpf_dec_batch(fmt, din, size, doff, 1, n, dv, d1 ? dstart : nullptr, nullptr, c.stream), "tpf_dec_batch");
+    void * hv = c.h_vals.get(vbytes);
+    hip_check(hipMemcpyAsync(hv, dv, es * written, hipMemcpyDeviceToHost, c.stream), "D2H values");
+    hip_check(hipStreamSynchronize(c.stream), "sync");
+    std::memcpy(out, hv, es * written);
+    return in + size;
+}
+
+} // namespace
+
+namespace tpf
+{
+void set_last_error(const std::string & msg);
+}
+
+namespace
+{
+
+template <class F>
+auto guarded(F && f) -> decltype(f())
+{
+    try
+    {
+        return f();
+    }
+    catch (const std::exception & e)
+    {
+        tpf::set_last_error(e.what());
+        std::fprintf(stderr, "%s\n", e.what());
+        return nullptr;
+    }
+}
+
+} // namespace
+
+// ---------------------------------------------------------------- turbopfor::
+namespace turbopfor
+{
+unsigned char * p4Enc32(uint32_t * in, unsigned n, unsigned char * out) { return enc_one(TPF_FMT_32, in, n, out, false, 0); }
+unsigned char * p4D1Enc32(uint32_t * in, unsigned n, unsigned char * out, uint32_t start)
+{
+    return enc_one(TPF_FMT_32, in, n, out, true, start);
+}
+const unsigned char * p4Dec32(const unsigned char * in, unsigned n, uint32_t * out) { return dec_one(TPF_FMT_32, in, n, out, false, 0); }
+const unsigned char * p4D1Dec32(const unsigned char * in, unsigned n, uint32_t * out, uint32_t start)
+{
+    return dec_one(TPF_FMT_32, in, n, out, true, start);
+}
+
+unsigned char * p4Enc128v32(uint32_t * in, unsigned n, unsigned char * out) { return enc_one(TPF_FMT_128V32, in, n, out, false, 0); }
+unsigned char * p4D1Enc128v32(uint32_t * in, unsigned n, unsigned char * out, uint32_t start)
+{
+    return enc_one(TPF_FMT_128V32, in, n, out, true, start);
+}
+const unsigned char * p4Dec128v32(const unsigned char * in, unsigned n, uint32_t * out)
+{
+    return dec_one(TPF_FMT_128V32, in, n, out, false, 0);
+}
+const unsigned char * p4D1Dec128v32(const unsigned char * in, unsigned n, uint32_t * out, uint32_t start)
+{
+    return dec_one(TPF_FMT_128V32, in, n, out, true, start);
+}
+
+unsigned char * p4Enc256v32(uint32_t * in, unsigned n, unsigned char * out) { return enc_one(TPF_FMT_256V32, in, n, out, false, 0); }
+unsigned char * p4D1Enc256v32(uint32_t * in, unsigned n, unsigned char * out, uint32_t start)
+{
+    return enc_one(TPF_FMT_256V32, in, n, out, true, start);
+}
+const unsigned char * p4Dec256v32(const unsigned char * in, unsigned n, uint32_t * out)
+{
+    return dec_one(TPF_FMT_256V32, in, n, out, false, 0);
+}
+const unsigned char * p4D1Dec256v32(const unsigned char * in, unsigned n, uint32_t * out, uint32_t start)
+{
+    return dec_one(TPF_FMT_256V32, in, n, out, true, start);
+}
+
+unsigned char * p4Enc64(uint64_t * in, unsigned n, unsigned char * out) { return enc_one(TPF_FMT_64, in, n, out, false, 0); }
+unsigned char * p4D1Enc64(uint64_t * in, unsigned n, unsigned char * out, uint64_t start)
+{
+    return enc_one(TPF_FMT_64, in, n, out, true, start);
+}
+const unsigned char * p4Dec64(const unsigned char * in, unsigned n, uint64_t * out) { return dec_one(TPF_FMT_64, in, n, out, false, 0); }
+const unsigned char * p4D1Dec64(const unsigned char * in, unsigned n, uint64_t * out, uint64_t start)
+{
+    return dec_one(TPF_FMT_64, in, n, out, true, start);
+}
+
+unsigned char * p4Enc128v64(uint64_t * in, unsigned n, unsigned char * out) { return enc_one(TPF_FMT_128V64, in, n, out, false, 0); }
+unsigned char * p4D1Enc128v64(uint64_t * in, unsigned n, unsigned char * out, uint64_t start)
+{
+    return enc_one(TPF_FMT_128V64, in, n, out, true, start);
+}
+const unsigned char * p4Dec128v64(const unsigned char * in, unsigned n, uint64_t * out)
+{
+    return dec_one(TPF_FMT_128V64, in, n, out, false, 0);
+}
+const unsigned char * p4D1Dec128v64(const unsigned char * in, unsigned n, uint64_t * out, uint64_t start)
+{
+    return dec_one(TPF_FMT_128V64, in, n, out, true, start);
+}
+
+unsigned char * p4Enc256v64(uint64_t * in, unsigned n, unsigned char * out) { return enc_one(TPF_FMT_256V64, in, n, out, false, 0); }
+unsigned char * p4D1Enc256v64(uint64_t * in, unsigned n, unsigned char * out, uint64_t start)
+{
+    return enc_one(TPF_FMT_256V64, in, n, out, true, start);
+}
+const unsigned char * p4Dec256v64(const unsigned char * in, unsigned n, uint64_t * out)
+{
+    return dec_one(TPF_FMT_256V64, in, n, out, false, 0);
+}
+const unsigned char * p4D1Dec256v64(const unsigned char * in, unsigned n, uint64_t * out, uint64_t start)
+{
+    return dec_one(TPF_FMT_256V64, in, n, out, true, start);
+}
+} // namespace turbopfor
+
+// ----------------------------------------------------------- extern "C" mirror
+extern "C" {
+
+#define TPF_MIRROR_ENC(NAME, T)                                                                                  \
+    unsigned char * tpf_##NAME(T * in, unsigned n, unsigned char * out)                                          \
+    {                                                                                                            \
+        return guarded([&]() -> unsigned char * { return turbopfor::NAME(in, n, out); });                      \
+    }
+#define TPF_MIRROR_D1ENC(NAME, T)                                                                                \
+    unsigned char * tpf_##NAME(T * in, unsigned n, unsigned char * out, T start)                                 \
+    {                                                                                                            \
+        return guarded([&]() -> unsigned char * { return turbopfor::NAME(in, n, out, start); });               \
+    }
+#define TPF_MIRROR_DEC(NAME, T)                                                                                  \
+    const unsigned char * tpf_##NAME(const unsigned char * in, unsigned n, T * out)                              \
+    {                                                                                                            \
+        return guarded([&]() -> const unsigned char * { return turbopfor::NAME(in, n, out); });                \
+    }
+#define TPF_MIRROR_D1DEC(NAME, T)                                                                                \
+    const unsigned char * tpf_##NAME(const unsigned char * in, unsigned n, T * out, T start)                     \
+    {                                                                                                            \
+        return guarded([&]() -> const unsigned char * { return turbopfor::NAME(in, n, out, start); });         \
+    }
+
+TPF_MIRROR_ENC(p4Enc32, uint32_t)
+TPF_MIRROR_D1ENC(p4D1Enc32, uint32_t)
+TPF_MIRROR_DEC(p4Dec32, uint32_t)
+TPF_MIRROR_D1DEC(p4D1Dec32, uint32_t)
+TPF_MIRROR_ENC(p4Enc128v32, uint32_t)
+TPF_MIRROR_D1ENC(p4D1Enc128v32, uint32_t)
+TPF_MIRROR_DEC(p4Dec128v32, uint32_t)
+TPF_MIRROR_D1DEC(p4D1Dec128v32, uint32_t)
+TPF_MIRROR_ENC(p4Enc256v32, uint32_t)
+TPF_MIRROR_D1ENC(p4D1Enc256v32, uint32_t)
+TPF_MIRROR_DEC(p4Dec256v32, uint32_t)
+TPF_MIRROR_D1DEC(p4D1Dec256v32, uint32_t)
+TPF_MIRROR_ENC(p4Enc64, uint64_t)
+TPF_MIRROR_D1ENC(p4D1Enc64, uint64_t)
+TPF_MIRROR_DEC(p4Dec64, uint64_t)
+TPF_MIRROR_D1DEC(p4D1Dec64, uint64_t)
+TPF_MIRROR_ENC(p4Enc128v64, uint64_t)
+TPF_MIRROR_D1ENC(p4D1Enc128v64, uint64_t)
+TPF_MIRROR_DEC(p4Dec128v64, uint64_t)
+TPF_MIRROR_D1DEC(p4D1Dec128v64, uint64_t)
+TPF_MIRROR_ENC(p4Enc256v64, uint64_t)
+TPF_MIRROR_D1ENC(p4D1Enc256v64, uint64_t)
+TPF_MIRROR_DEC(p4Dec256v64, uint64_t)
+TPF_MIRROR_D1DEC(p4D1Dec256v64, uint64_t)
+
+} // extern "C"

@@ -148,7 +148,7 @@ namespace tpf
 size_t enc256v32_workspace(uint64_t nblocks)
 {
     size_t scan_bytes = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, static_cast<uint64_t *>(nullptr),
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, static_cast<uint64_t *>(nullptr),
                                      static_cast<int>(std::min<uint64_t>(nblocks + 1, 0x7FFFFFFF)));
     return ((nblocks * 4u + 255u) & ~size_t(255)) + scan_bytes + 256;
 }

@@ -392,7 +392,6 @@ template <Fmt F>
 __device__ __forceinline__ PlanG plan_block_g(const typename FmtTraits<F>::T v[4], uint32_t n, uint32_t * hist, uint32_t t)
 {
     using Tr = FmtTraits<F>;
-    using T = typename Tr::T;
     constexpr uint32_t W = Tr::W;
     constexpr bool wide = Tr::wide;
     const uint32_t NE = Tr::N ? Tr::N : n;
@@ -549,6 +548,7 @@ __device__ __forceinline__ void emit_block_g(uint32_t * img, uint32_t s, const P
     constexpr bool wide = Tr::wide;
     const uint32_t NE = Tr::N ? Tr::N : n;
     const uint32_t b = P.b;
+    (void)sizeof(typename Tr::T);
     const uint32_t bh = (wide && b >= 64u) ? 63u : b;
     if (P.bx == 0u)
     {

@@ -267,7 +267,7 @@ hipError_t enc_fmt(const void * in, uint64_t nblocks, uint32_t n, bool d1, const
 size_t generic_workspace(uint64_t nblocks)
 {
     size_t scan_bytes = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, static_cast<uint64_t *>(nullptr),
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, static_cast<uint64_t *>(nullptr),
                                      static_cast<int>(std::min<uint64_t>(nblocks + 1, 0x7FFFFFFF)));
     return scan_bytes + 256;
 }
