@@ -51,6 +51,25 @@ int tpf_p4dec256v32_batch(const uint8_t *d_in, uint64_t in_bytes, const uint64_t
 int tpf_p4d1dec256v32_batch(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks,
                             uint32_t *d_out, const uint32_t *d_starts, uint64_t *d_err, void *stream);
 
+/* ---- 256v32 chained delta-1 decode -------------------
+ * One posting list split into nblocks consecutive 256v32 D1 blocks, encoded
+ * the way reference callers chain them (start of block i = last value of
+ * block i-1, README.md:116-123): decode the whole list on the device with
+ * only the list's initial start0.  Phase A (chain_sums) decodes every block's
+ * delta sum and prefix-sums them into the workspace; phase B (chain_decode)
+ * decodes with start(i) = base + prefix(i-1).  tpf_p4d1dec256v32_chained = A+B
+ * with base = start0.  For a list sharded over GPUs, each rank runs A, the
+ * ranks exchange their totals (d_total, one u32 each) and each runs B with
+ * base = start0 + the totals of all earlier shards (mod 2^32). */
+size_t tpf_p4d1dec256v32_chain_workspace_size(uint64_t nblocks);
+int tpf_p4d1dec256v32_chained(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks,
+                              uint32_t *d_out, uint32_t start0, void *d_ws, size_t ws_bytes, uint64_t *d_err,
+                              void *stream);
+int tpf_p4d1dec256v32_chain_sums(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks,
+                                 void *d_ws, size_t ws_bytes, uint32_t *d_total, uint64_t *d_err, void *stream);
+int tpf_p4d1dec256v32_chain_decode(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks,
+                                   uint32_t *d_out, uint32_t base, const void *d_ws, uint64_t *d_err, void *stream);
+
 /* ---- 256v32 encode ---------------------------------------------------
  * Replaces turbopfor::p4Enc256v32 (include/turbopfor.h:33, dispatch.cpp:70-77)
  * and p4D1Enc256v32 (:36, dispatch.cpp:79-86) for nblocks blocks of 256

@@ -1,0 +1,80 @@
+"""world_size-2 gloo tests of the multi-GPU path (tpf_shard), run on CPU:
+sharding + offset rebasing, and the one real exchange step (delta-1 list
+chained across shards), with the oracle standing in for the per-shard GPU
+decode."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import datagen
+import oracle_lib
+import tpf_shard
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        vals, starts = datagen.c3_postings(600, seed=11)
+        start0 = 12345
+        vals = (vals.astype(np.uint64) + start0).astype(np.uint32)  # list continues after start0
+        starts = np.concatenate([[start0], vals[:-1, -1]]).astype(np.uint32)
+        packed, off = oracle_lib.enc256v32_batch(vals, starts=starts)  # chained D1 encoding
+        lo, hi = tpf_shard.shard_range(len(vals), world, rank)
+        loff, (b0, b1) = tpf_shard.rebase(off, lo, hi)
+        shard = packed[b0:b1]
+        # phase A on this shard: delta sums per block (decode with start 0, last value = total)
+        raw = oracle_lib.dec256v32_batch(shard, loff, hi - lo, starts=np.zeros(hi - lo, np.uint32))
+        sums = ((raw[:, -1].astype(np.uint64)) & 0xFFFFFFFF).astype(np.uint64)
+        local_total = int(sums.sum() & 0xFFFFFFFF)
+        base = tpf_shard.chained_base(torch.tensor([local_total]), start0=start0)
+        # phase B: per-block starts from base + local prefix
+        pref = np.concatenate([[0], np.cumsum(sums)[:-1]]).astype(np.uint64)
+        bst = ((pref + base) & 0xFFFFFFFF).astype(np.uint32)
+        got = oracle_lib.dec256v32_batch(shard, loff, hi - lo, starts=bst)
+        ok = np.array_equal(got, vals[lo:hi])
+        ok_all = tpf_shard.all_ok(ok, "cpu")
+        tmax = tpf_shard.max_over_ranks(float(rank + 1), "cpu")
+        q.put((rank, ok, ok_all, tmax, (lo, hi)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_chained_d1_across_two_ranks():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    assert [r[1] for r in res] == [True, True]
+    assert all(r[2] for r in res)
+    assert all(r[3] == 2.0 for r in res)
+    assert res[0][4] == (0, 300) and res[1][4] == (300, 600)
+
+
+def test_shard_range_covers():
+    for n in (1, 7, 100, 80_000_000):
+        for w in (1, 2, 3, 8):
+            rs = [tpf_shard.shard_range(n, w, r) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))

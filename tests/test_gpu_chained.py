@@ -1,0 +1,53 @@
+"""Chained delta-1 decode (one posting list over many 256v32 blocks, only the
+list's start given) on the GPU, single shard and simulated multi-shard
+exchange, against the original values (bit-exact)."""
+import numpy as np
+import pytest
+
+import datagen
+import oracle_lib
+
+torch = pytest.importorskip("torch")
+tpf = pytest.importorskip("turbopfor_amd")
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _list(nb, start0, seed):
+    vals, _ = datagen.c3_postings(nb, seed=seed)
+    vals = (vals.astype(np.uint64) + start0 + 1).astype(np.uint32)
+    starts = np.concatenate([[start0], vals[:-1, -1]]).astype(np.uint32)
+    return vals, starts
+
+
+@pytest.mark.parametrize("start0", [0, 7, 0xFFFFFF00])
+def test_chained_single(start0):
+    vals, starts = _list(5000, start0, seed=3)
+    packed_np, off_np = oracle_lib.enc256v32_batch(vals, starts=starts)
+    packed = torch.from_numpy(packed_np).to(DEV)
+    offs = torch.from_numpy(off_np.astype(np.int64)).to(DEV)
+    err = torch.zeros(1, dtype=torch.int64, device=DEV)
+    out = tpf.dec256v32_chained(packed, offs, len(vals), start0=start0, err=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == -1
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), vals)
+
+
+def test_chained_sharded_exchange():
+    import tpf_shard
+
+    start0 = 99
+    vals, starts = _list(7001, start0, seed=4)
+    packed_np, off_np = oracle_lib.enc256v32_batch(vals, starts=starts)
+    world = 3
+    chains, totals = [], []
+    for r in range(world):
+        lo, hi = tpf_shard.shard_range(len(vals), world, r)
+        loff, (b0, b1) = tpf_shard.rebase(off_np.astype(np.int64), lo, hi)
+        c = tpf.D1Chain(torch.from_numpy(packed_np[b0:b1].copy()).to(DEV), torch.from_numpy(loff).to(DEV), hi - lo)
+        totals.append(int(c.sums().item()) & 0xFFFFFFFF)
+        chains.append((c, lo, hi))
+    for r, (c, lo, hi) in enumerate(chains):
+        base = (start0 + sum(totals[:r])) & 0xFFFFFFFF
+        out = c.decode(base)
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), vals[lo:hi], err_msg=f"shard {r}")

@@ -1,116 +1,40 @@
 // p4_dec256v32.hip -- batch decode of 256v32 P4 blocks (p4Dec256v32 /
 // p4D1Dec256v32, reference src/scalar/p4dec256v32_scalar.cpp:90-137 and
-// p4d1dec256v32_scalar.cpp:198-268) on gfx950.
+// p4d1dec256v32_scalar.cpp:198-268) on gfx950: the hot path.
 //
-// Geometry: a 256-thread workgroup walks tiles of kTile consecutive blocks
-// (grid-stride).  Because the blocks of a tile are contiguous in the packed
-// stream, the whole tile [off[i0], off[i0+kTile]) is staged into LDS with one
-// coalesced sweep of 16-byte buffer loads (the bytes of ~8 blocks in flight
-// per workgroup), then each wave decodes blocks w, w+4 of the tile from LDS
-// and writes 1 KB per block with one global_store_dwordx4 per lane.  Tiles
-// larger than the staging area (only possible with vbyte-heavy blocks) fall
-// back to per-wave staging of single blocks.
+// Design notes (measured on MI355X): a first version staged
+// tiles of 8 consecutive blocks per workgroup with one coalesced sweep and
+// __syncthreads; it was latency-bound (one tile in flight per workgroup,
+// 39% of HBM peak).  The kernel below runs every wave independently with a
+// software pipeline and no workgroup barrier.
 #include "p4_block32.h"
 #include "tpf_kernels.h"
 
-#include <cstdlib>
+#include <hipcub/hipcub.hpp>
 
 namespace tpf::dev
 {
 
-constexpr uint32_t kTile = 8;             // blocks per workgroup tile
-constexpr uint32_t kStage = 10240;        // staging bytes per workgroup
-constexpr uint32_t kWaveSlot = kStage / 4; // per-wave staging in the fallback
-constexpr uint32_t kWG = 256;
-
 enum class StartMode : int
 {
     None = 0,     // p4Dec256v32
-    PerBlock = 1, // p4D1Dec256v32 with starts[i]
+    PerBlock = 1, // p4D1Dec256v32, start of block i = starts[i]
+    Prefix = 2,   // chained list: start of block i = base + incl[i-1] (incl = prefix of block sums)
+    SumOnly = 3,  // no output: sums[i] = sum over the block of (v + 1) mod 2^32
 };
 
-template <StartMode SM>
-__global__ __launch_bounds__(256) void k_dec256v32(const uint8_t * __restrict in, uint64_t in_bytes,
-                                                    const uint64_t * __restrict off, uint64_t nblocks,
-                                                    uint32_t * __restrict out, const uint32_t * __restrict starts,
-                                                    unsigned long long * __restrict err)
+struct DecArgs
 {
-    __shared__ uint32_t stage[(kStage + 64) / 4];
-    __shared__ uint32_t scratch[4 * kWaveScratchU32];
-    __shared__ uint64_t toff[kTile + 1];
-
-    const uint32_t tid = threadIdx.x;
-    const uint32_t t = tid & 63u;
-    const uint32_t wv = uni(tid >> 6);
-    uint32_t * scr = scratch + wv * kWaveScratchU32;
-    const uint64_t ntiles = (nblocks + kTile - 1) / kTile;
-    const uint64_t in_base = reinterpret_cast<uint64_t>(in);
-    const uint64_t in_end = in_base + in_bytes;
-
-    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x)
-    {
-        const uint64_t i0 = tile * kTile;
-        const uint32_t nb = static_cast<uint32_t>(min_u64(kTile, nblocks - i0));
-        if (tid <= nb)
-            toff[tid] = off[i0 + tid];
-        __syncthreads();
-        const uint64_t a0 = (in_base + toff[0]) & ~15ull;
-        const uint64_t aend = in_base + toff[nb];
-        const uint64_t span = aend > a0 ? aend - a0 : 0;
-
-        if (span <= kStage)
-        {
-            const uint32_t avail = static_cast<uint32_t>(min_u64(in_end > a0 ? in_end - a0 : 0, kStage));
-            const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(a0), avail);
-            for (uint32_t x = tid * 16u; x < span; x += kWG * 16u)
-                *reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(stage) + x) =
-                    load16_guarded(reinterpret_cast<const uint8_t *>(a0), rs, x, avail);
-            __syncthreads();
-            for (uint32_t j = wv; j < nb; j += 4)
-            {
-                const uint64_t bo = toff[j];
-                const uint32_t s = static_cast<uint32_t>(in_base + bo - a0);
-                u32x4 v;
-                const uint32_t used = decode_block256v32(stage, s, scr, t, v);
-                const uint64_t blk = i0 + j;
-                if constexpr (SM == StartMode::PerBlock)
-                    apply_delta1_256(v, starts[blk]);
-                reinterpret_cast<u32x4 *>(out + blk * 256u)[t] = v;
-                if (err != nullptr && t == 0 && static_cast<uint64_t>(used) != toff[j + 1] - bo)
-                    atomicMin(err, static_cast<unsigned long long>(blk));
-            }
-        }
-        else
-        {
-            // Fallback: each wave stages one block at a time into its quarter.
-            uint32_t * slot = stage + wv * (kWaveSlot / 4);
-            for (uint32_t j = wv; j < nb; j += 4)
-            {
-                const uint64_t babs = in_base + toff[j];
-                const uint64_t ba = babs & ~15ull;
-                const uint64_t bend = in_base + toff[j + 1];
-                const uint32_t bspan = static_cast<uint32_t>(min_u64(bend > ba ? bend - ba : 0, kWaveSlot - 64));
-                const uint32_t avail = static_cast<uint32_t>(min_u64(in_end > ba ? in_end - ba : 0, kWaveSlot - 64));
-                const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(ba), avail);
-                for (uint32_t x = t * 16u; x < bspan; x += kWave * 16u)
-                    *reinterpret_cast<u32x4 *>(reinterpret_cast<uint8_t *>(slot) + x) =
-                        load16_guarded(reinterpret_cast<const uint8_t *>(ba), rs, x, avail);
-                wave_lds_sync();
-                u32x4 v;
-                const uint32_t used = decode_block256v32(slot, static_cast<uint32_t>(babs - ba), scr, t, v);
-                const uint64_t blk = i0 + j;
-                if constexpr (SM == StartMode::PerBlock)
-                    apply_delta1_256(v, starts[blk]);
-                reinterpret_cast<u32x4 *>(out + blk * 256u)[t] = v;
-                if (err != nullptr && t == 0 && static_cast<uint64_t>(used) != toff[j + 1] - toff[j])
-                    atomicMin(err, static_cast<unsigned long long>(blk));
-                wave_lds_sync();
-            }
-        }
-        __syncthreads();
-    }
-}
-
+    const uint8_t * in;
+    uint64_t in_bytes;
+    const uint64_t * off;
+    uint64_t nblocks;
+    uint32_t * out;
+    const uint32_t * starts; // PerBlock: starts; Prefix: inclusive block-sum prefix
+    uint32_t base;           // Prefix: value preceding block 0
+    uint32_t * sums;         // SumOnly
+    unsigned long long * err;
+};
 
 // ---------------------------------------------------------------------------
 // Wave-independent variant: every wave owns a private LDS slot and walks
@@ -151,8 +75,7 @@ __device__ __forceinline__ void issue_chunk(Chunk & c, uint64_t in_base, uint64_
 
 template <StartMode SM>
 __device__ __forceinline__ bool consume_chunk(const Chunk & c, uint64_t in_base, uint64_t o, uint64_t e, uint64_t blk,
-                                              uint32_t * slot, uint32_t * scr, uint32_t * __restrict out,
-                                              const uint32_t * __restrict starts, uint32_t t)
+                                              uint32_t * slot, uint32_t * scr, const DecArgs & A, uint32_t t)
 {
     reinterpret_cast<u32x4 *>(slot)[t] = c.a;
     if (c.span > 1024u)
@@ -169,9 +92,20 @@ __device__ __forceinline__ bool consume_chunk(const Chunk & c, uint64_t in_base,
     wave_lds_sync();
     u32x4 v;
     const uint32_t used = decode_block256v32(slot, static_cast<uint32_t>(in_base + o - c.base), scr, t, v);
-    if constexpr (SM == StartMode::PerBlock)
-        apply_delta1_256(v, starts[blk]);
-    reinterpret_cast<u32x4 *>(out + blk * 256u)[t] = v;
+    if constexpr (SM == StartMode::SumOnly)
+    {
+        const uint32_t s = wave_sum(v.x + v.y + v.z + v.w + 4u);
+        if (t == 0)
+            A.sums[blk] = s;
+    }
+    else
+    {
+        if constexpr (SM == StartMode::PerBlock)
+            apply_delta1_256(v, A.starts[blk]);
+        if constexpr (SM == StartMode::Prefix)
+            apply_delta1_256(v, A.base + (blk ? A.starts[blk - 1] : 0u));
+        reinterpret_cast<u32x4 *>(A.out + blk * 256u)[t] = v;
+    }
     wave_lds_sync();
     return static_cast<uint64_t>(used) == e - o;
 }
@@ -192,11 +126,12 @@ __device__ __forceinline__ uint64_t lane_u64(uint64_t v, uint32_t lane)
 }
 
 template <StartMode SM>
-__global__ __launch_bounds__(256) void k_dec256v32w(const uint8_t * __restrict in, uint64_t in_bytes,
-                                                     const uint64_t * __restrict off, uint64_t nblocks,
-                                                     uint32_t * __restrict out, const uint32_t * __restrict starts,
-                                                     unsigned long long * __restrict err)
+__global__ __launch_bounds__(256) void k_dec256v32w(const DecArgs A)
 {
+    const uint8_t * in = A.in;
+    const uint64_t in_bytes = A.in_bytes;
+    const uint64_t * off = A.off;
+    const uint64_t nblocks = A.nblocks;
     __shared__ uint32_t slots[4][kSlotBytes / 4];
     __shared__ uint32_t scratch[4][kWaveScratchU32];
     const uint32_t t = threadIdx.x & 63u;
@@ -222,7 +157,7 @@ __global__ __launch_bounds__(256) void k_dec256v32w(const uint8_t * __restrict i
     };
     auto consume = [&](const Chunk & c, uint32_t jj) {
         const uint64_t o = lane_u64(offv, jj), e = lane_u64(offv, jj + 1);
-        if (!consume_chunk<SM>(c, in_base, o, e, first + jj, slot, scr, out, starts, t))
+        if (!consume_chunk<SM>(c, in_base, o, e, first + jj, slot, scr, A, t))
             bad = min_u64(bad, first + jj);
     };
     issue(C0, 0);
@@ -242,8 +177,8 @@ __global__ __launch_bounds__(256) void k_dec256v32w(const uint8_t * __restrict i
         if (j + 3 >= n)
             break;
     }
-    if (err != nullptr && t == 0 && bad != ~0ull)
-        atomicMin(err, static_cast<unsigned long long>(bad));
+    if (A.err != nullptr && t == 0 && bad != ~0ull)
+        atomicMin(A.err, static_cast<unsigned long long>(bad));
 }
 
 } // namespace tpf::dev
@@ -251,36 +186,61 @@ __global__ __launch_bounds__(256) void k_dec256v32w(const uint8_t * __restrict i
 namespace tpf
 {
 
+namespace
+{
+template <dev::StartMode SM>
+hipError_t launch_mode(const dev::DecArgs & A, hipStream_t stream)
+{
+    const uint64_t per_wg = 4ull * dev::kRun;
+    const uint32_t grid = static_cast<uint32_t>((A.nblocks + per_wg - 1) / per_wg);
+    hipLaunchKernelGGL(dev::k_dec256v32w<SM>, dim3(grid), dim3(256), 0, stream, A);
+    return hipGetLastError();
+}
+} // namespace
+
 hipError_t launch_dec256v32(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * out,
                             const uint32_t * starts, unsigned long long * err, hipStream_t stream)
 {
     if (nblocks == 0)
         return hipSuccess;
-    static const int variant = [] {
-        const char * e = std::getenv("TPF_DEC_VARIANT");
-        return e ? std::atoi(e) : 1;
-    }();
-    if (variant == 1)
-    {
-        const uint64_t per_wg = 4ull * dev::kRun;
-        const uint32_t grid = static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg);
-        if (starts)
-            hipLaunchKernelGGL(dev::k_dec256v32w<dev::StartMode::PerBlock>, dim3(grid), dim3(256), 0, stream, in, in_bytes,
-                               off, nblocks, out, starts, err);
-        else
-            hipLaunchKernelGGL(dev::k_dec256v32w<dev::StartMode::None>, dim3(grid), dim3(256), 0, stream, in, in_bytes, off,
-                               nblocks, out, starts, err);
-        return hipGetLastError();
-    }
-    const uint64_t ntiles = (nblocks + dev::kTile - 1) / dev::kTile;
-    const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(ntiles, grid_cap(stream, 8)));
-    if (starts)
-        hipLaunchKernelGGL(dev::k_dec256v32<dev::StartMode::PerBlock>, dim3(grid), dim3(dev::kWG), 0, stream, in, in_bytes,
-                           off, nblocks, out, starts, err);
-    else
-        hipLaunchKernelGGL(dev::k_dec256v32<dev::StartMode::None>, dim3(grid), dim3(dev::kWG), 0, stream, in, in_bytes, off,
-                           nblocks, out, starts, err);
-    return hipGetLastError();
+    const dev::DecArgs A{in, in_bytes, off, nblocks, out, starts, 0u, nullptr, err};
+    return starts ? launch_mode<dev::StartMode::PerBlock>(A, stream) : launch_mode<dev::StartMode::None>(A, stream);
+}
+
+// Chained delta-1: phase A computes every block's sum of
+// (v+1) and their inclusive prefix in `incl` (device, nblocks u32); phase B
+// decodes with start(i) = base + incl[i-1].  A shard of a multi-GPU list runs
+// A, exchanges its total incl[n-1] with the other ranks, then B with its base.
+size_t d1chain_workspace(uint64_t nblocks)
+{
+    size_t scan_bytes = 0;
+    (void)hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes, static_cast<uint32_t *>(nullptr), static_cast<uint32_t *>(nullptr),
+                                           static_cast<int>(std::min<uint64_t>(nblocks, 0x7FFFFFFF)));
+    return scan_bytes + 256;
+}
+
+hipError_t launch_d1chain_sums(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * incl,
+                               void * ws, size_t ws_bytes, unsigned long long * err, hipStream_t stream)
+{
+    if (nblocks == 0)
+        return hipSuccess;
+    if (nblocks > 0x7FFFFFFFull)
+        return hipErrorInvalidValue;
+    const dev::DecArgs A{in, in_bytes, off, nblocks, nullptr, nullptr, 0u, incl, err};
+    hipError_t e = launch_mode<dev::StartMode::SumOnly>(A, stream);
+    if (e != hipSuccess)
+        return e;
+    size_t sb = ws_bytes;
+    return hipcub::DeviceScan::InclusiveSum(ws, sb, incl, incl, static_cast<int>(nblocks), stream);
+}
+
+hipError_t launch_d1chain_decode(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * out,
+                                 const uint32_t * incl, uint32_t base, unsigned long long * err, hipStream_t stream)
+{
+    if (nblocks == 0)
+        return hipSuccess;
+    const dev::DecArgs A{in, in_bytes, off, nblocks, out, incl, base, nullptr, err};
+    return launch_mode<dev::StartMode::Prefix>(A, stream);
 }
 
 } // namespace tpf

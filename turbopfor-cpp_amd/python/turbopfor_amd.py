@@ -59,8 +59,15 @@ def lib():
         L.tpf_dec_batch.argtypes = [ctypes.c_int, c_vp, c_u64, c_vp, c_u64, ctypes.c_uint, c_vp, c_vp, c_vp, c_vp]
         L.tpf_enc_batch.argtypes = [ctypes.c_int, c_vp, c_u64, ctypes.c_uint, ctypes.c_int, c_vp, c_u64, c_vp, c_u64,
                                     c_vp, c_vp, ctypes.c_size_t, c_vp]
+        L.tpf_p4d1dec256v32_chain_workspace_size.argtypes = [c_u64]
+        L.tpf_p4d1dec256v32_chain_workspace_size.restype = ctypes.c_size_t
+        L.tpf_p4d1dec256v32_chained.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, ctypes.c_uint32, c_vp, ctypes.c_size_t,
+                                                c_vp, c_vp]
+        L.tpf_p4d1dec256v32_chain_sums.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, ctypes.c_size_t, c_vp, c_vp, c_vp]
+        L.tpf_p4d1dec256v32_chain_decode.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, ctypes.c_uint32, c_vp, c_vp, c_vp]
         for name in ("tpf_p4dec256v32_batch", "tpf_p4d1dec256v32_batch", "tpf_p4enc256v32_batch",
-                     "tpf_p4d1enc256v32_batch", "tpf_dec_batch", "tpf_enc_batch"):
+                     "tpf_p4d1enc256v32_batch", "tpf_dec_batch", "tpf_enc_batch", "tpf_p4d1dec256v32_chained",
+                     "tpf_p4d1dec256v32_chain_sums", "tpf_p4d1dec256v32_chain_decode"):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -170,3 +177,47 @@ def dec_batch(fmt, packed, offsets, nblocks, n, starts=None, err=None, out=None)
                          _ptr(err), _stream(torch))
     _check(rc)
     return out
+
+
+# ---- chained delta-1 decode of one posting list (f1) ----------------------
+class D1Chain:
+    """Two-phase chained p4D1Dec256v32 over one list: sums() decodes every
+    block's delta sum and its prefix (returns the shard total as a 1-element
+    int32 CUDA tensor), decode(base) writes the values.  A multi-GPU list
+    runs sums() on every shard, exchanges the totals, then decode() with
+    base = start0 + sum of earlier shards' totals (mod 2^32)."""
+
+    def __init__(self, packed, offsets, nblocks):
+        import torch
+
+        self.packed, self.offsets, self.nblocks = packed, offsets, nblocks
+        L = lib()
+        self.ws_bytes = int(L.tpf_p4d1dec256v32_chain_workspace_size(nblocks))
+        self.ws = torch.empty(max(self.ws_bytes, 1), dtype=torch.uint8, device=packed.device)
+        self.total = torch.zeros(1, dtype=torch.int32, device=packed.device)
+
+    def sums(self, err=None):
+        import torch
+
+        rc = lib().tpf_p4d1dec256v32_chain_sums(_ptr(self.packed), self.packed.numel(), _ptr(self.offsets), self.nblocks,
+                                                _ptr(self.ws), self.ws_bytes, _ptr(self.total), _ptr(err),
+                                                _stream(torch))
+        _check(rc)
+        return self.total
+
+    def decode(self, base, out=None, err=None):
+        import torch
+
+        if out is None:
+            out = torch.empty((self.nblocks, 256), dtype=torch.int32, device=self.packed.device)
+        rc = lib().tpf_p4d1dec256v32_chain_decode(_ptr(self.packed), self.packed.numel(), _ptr(self.offsets),
+                                                  self.nblocks, _ptr(out), ctypes.c_uint32(base & 0xFFFFFFFF),
+                                                  _ptr(self.ws), _ptr(err), _stream(torch))
+        _check(rc)
+        return out
+
+
+def dec256v32_chained(packed, offsets, nblocks, start0=0, out=None, err=None):
+    c = D1Chain(packed, offsets, nblocks)
+    c.sums(err=err)
+    return c.decode(start0, out=out)
