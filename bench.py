@@ -1,25 +1,32 @@
 #!/usr/bin/env python3
 """bench.py -- device-resident p4Dec256v32 throughput on MI355X.
 
-Workload (BASELINE.json configs[1], "C2"): 10M blocks of 256 uint32, bit
-widths 1..32 swept as 32 equal consecutive segments, 10% exceptions (bw<=28,
-benchmarks/ab_test.cpp:1448/1610-1631), synthetic data generated on the GPU.
-The packed stream is produced by our GPU encoder (untimed) and verified by a
-full-size round trip after the timed region.  One step = one
-tpf_p4dec256v32_batch launch over the whole shard (inputs resident in HBM).
+Default workload (BASELINE.json configs[1], "C2"): 10M blocks of 256 uint32
+per GPU, bit widths 1..32 swept as 32 equal consecutive segments, 10%
+exceptions (bw <= 28; benchmarks/ab_test.cpp:1448, :1610-1631), synthetic data
+generated on the GPU.  The packed stream is produced by our GPU encoder
+(untimed; parity-tested against the reference-pinned oracle) and the timed
+decode is verified bit-exact at full size afterwards.  One step = one
+tpf_p4dec256v32_batch launch over the whole shard, inputs resident in HBM.
 
-Multi-GPU (torchrun, one process per GPU): every rank decodes its own 10M-block
-shard (weak scaling, no collective on the data path); RCCL only carries the
-barrier and the max-over-ranks time.
+Other workloads (--workload, one JSON line each, for DESIGN.md):
+  c3      p4D1Dec256v32 on Zipf posting lists (5% big gaps), per-block starts
+  c3chain the same list decoded as ONE chained list (only start0 given)
+  c4      p4Enc256v32 + p4Dec256v32 round trip (0/5/10/25% exceptions) and
+          the 256v64 round trip (bw 1..64 with exceptions above bit 32)
+--e2e adds the host-memory rate (pinned H2D + decode + D2H, tpf_host_dec).
 
-Prints ONE JSON line on rank 0 (see the driver contract in the task prompt),
-with a `roofline` object for the decode kernel and a `cpu_baseline` object
-(the reference library compiled from /root/reference, run on this host's CPU
-on a bounded sample of the same workload).
+Multi-GPU (torchrun, one process per GPU): every rank owns its own shard
+(weak scaling); the decode needs no collective.  RCCL carries the barrier,
+the max-over-ranks time and, for c3chain, the one real exchange step (each
+shard's delta total, tpf_shard.chained_base).
+
+Rank 0 prints ONE JSON line with `roofline` (decode kernel, HIP events on
+the launch stream) and `cpu_baseline` (the reference library compiled from
+its own sources, run on this host's cores on a bounded sample).
 """
 import argparse
 import ctypes
-import glob
 import json
 import os
 import sys
@@ -30,19 +37,28 @@ import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "turbopfor-cpp_amd", "python"))
+import tpf_shard  # noqa: E402
 import turbopfor_amd as tpf  # noqa: E402
 
 METRIC = "G int32/s device-resident p4Dec256v32 (+ compressed GB/s vs HBM peak)"
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def as_i32(v64):
+    """uint32 values held in int64 -> int32 bit patterns."""
+    return (v64 - ((v64 >> 31) << 32)).to(torch.int32)
+
+
 # --------------------------------------------------------------- data (GPU)
-def gen_c2(nblocks, exc_pct, seed, dev):
-    """uint32 bit patterns (as int32) [nblocks, 256]; 32 equal segments, bw 1..32."""
+def gen_c2(nblocks, exc_pct, seed, dev, pcts=None):
+    """[nblocks, 256] uint32 bit patterns: 32 equal segments with bw 1..32,
+    exceptions U[2^bw, 2^32) with probability exc_pct (or pcts cycling per
+    segment) for bw <= 28."""
     vals = torch.empty((nblocks, 256), dtype=torch.int32, device=dev)
     seg = [(nblocks * s) // 32 for s in range(33)]
     g = torch.Generator(device=dev)
@@ -51,56 +67,70 @@ def gen_c2(nblocks, exc_pct, seed, dev):
         lo, hi = seg[s], seg[s + 1]
         if hi <= lo:
             continue
+        pct = pcts[s % len(pcts)] if pcts else exc_pct
         g.manual_seed(seed * 1000 + bw)
         n = (hi - lo) * 256
         v = torch.randint(0, 1 << bw, (n,), device=dev, generator=g, dtype=torch.int64)
-        if exc_pct > 0 and bw <= 28:
-            m = torch.rand(n, device=dev, generator=g) < (exc_pct / 100.0)
+        if pct > 0 and bw <= 28:
+            m = torch.rand(n, device=dev, generator=g) < (pct / 100.0)
             e = torch.randint(1 << bw, 1 << 32, (n,), device=dev, generator=g, dtype=torch.int64)
             v = torch.where(m, e, v)
             del m, e
-        vals[lo:hi] = (v - ((v >> 31) << 32)).to(torch.int32).view(hi - lo, 256)
+        vals[lo:hi] = as_i32(v).view(hi - lo, 256)
         del v
     return vals, seg
 
 
-# --------------------------------------------------------- profile traffic
-def pmc_traffic(nblocks):
-    """HBM bytes per decode launch from the committed rocprofv3 PMC passes
-    (profiles/*pmc*.csv), corrected as MI355X_MICROARCH.md §HBM prescribes:
-    FETCH_SIZE and WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports half of a
-    wide coalesced stream, so it is doubled.  Returns None when no matching
-    profile exists."""
-    fetch, write = None, None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*_counter_collection.csv"))):
-        try:
-            import csv
+def gen_c3(nblocks, seed, dev):
+    """Sorted posting list: 95% gaps bounded Zipf(s=1.1) on [1,64], 5% gaps
+    64+U[0,2^16).  Returns values [nblocks,256] (int32 bit
+    patterns), per-block starts (value preceding each block; 0 for block 0)."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    n = nblocks * 256
+    vals = torch.empty(n, dtype=torch.int32, device=dev)
+    carry = 0
+    step = 64 << 20
+    for a in range(0, n, step):
+        m = min(step, n - a)
+        u = torch.rand(m, device=dev, generator=g, dtype=torch.float64)
+        s = 1.1
+        x = (1.0 + u * (65.0 ** (1 - s) - 1.0)) ** (1.0 / (1 - s))
+        gap = torch.clamp(torch.floor(x), 1, 64).to(torch.int64)
+        big = torch.rand(m, device=dev, generator=g) < 0.05
+        gap = torch.where(big, 64 + torch.randint(0, 1 << 16, (m,), device=dev, generator=g), gap)
+        cs = torch.cumsum(gap, 0) + carry
+        carry = int(cs[-1].item())
+        vals[a : a + m] = as_i32(cs & 0xFFFFFFFF)
+        del u, x, gap, big, cs
+    vals = vals.view(nblocks, 256)
+    starts = torch.zeros(nblocks, dtype=torch.int32, device=dev)
+    starts[1:] = vals[:-1, -1]
+    return vals, starts
 
-            with open(path) as f:
-                rows = [r for r in csv.DictReader(f) if "k_dec256v32" in r.get("Kernel_Name", "")]
-        except Exception:
-            continue
-        for name in ("FETCH_SIZE", "WRITE_SIZE"):
-            vals = [float(r["Counter_Value"]) for r in rows if r.get("Counter_Name") == name]
-            if vals:
-                med = float(np.median(vals))
-                if name == "FETCH_SIZE":
-                    fetch = med
-                else:
-                    write = med
-    if fetch is None or write is None:
+
+# --------------------------------------------------------- profile traffic
+def pmc_traffic(workload, nblocks):
+    """HBM bytes per decode launch measured with rocprofv3 PMC counters for
+    exactly this workload (profiles/pmc_traffic.json, written by
+    scripts/pmc_traffic.py: FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM
+    plus WRITE_SIZE, KiB -> bytes).  None when no matching measurement."""
+    try:
+        d = json.load(open(PROFILE_TRAFFIC))
+    except Exception:
         return None
-    return (2.0 * fetch + write) * 1024.0
+    if d.get("workload") != workload or int(d.get("nblocks", -1)) != nblocks:
+        return None
+    return d.get("hbm_bytes_per_launch")
 
 
 # ------------------------------------------------------------- cpu baseline
 def cpu_baseline(packed_host, off_host, nblocks, budget_s=12.0, threads=None):
-    """Reference library (oracle/_ref, compiled from the reference sources,
-    turbopfor::p4Dec256v32 = AVX2 dispatch path) decoding a bounded sample of
-    the same packed stream with `threads` std::threads; falls back to the
-    oracle restatement (kind "port") when _ref is absent."""
+    """Reference library (oracle/_ref: the reference's own sources compiled by
+    oracle/Makefile; turbopfor::p4Dec256v32 = its AVX2 dispatch path) decoding
+    a bounded sample of the same packed stream with `threads` std::threads.
+    Falls back to the oracle restatement (kind "port") if _ref is absent."""
     threads = threads or min(16, os.cpu_count() or 1)
-    # sample: the first 1/16 of every bw segment (contiguous bytes per segment)
     seg = [(nblocks * s) // 32 for s in range(33)]
     parts, offs = [], [np.zeros(1, dtype=np.uint64)]
     base = 0
@@ -113,8 +143,7 @@ def cpu_baseline(packed_host, off_host, nblocks, budget_s=12.0, threads=None):
         base += b1 - b0
     sample = np.concatenate(parts + [np.zeros(64, np.uint8)])
     soff = np.ascontiguousarray(np.concatenate(offs), dtype=np.uint64)
-    idx = np.arange(len(soff) - 1)
-    nb = len(idx)
+    nb = len(soff) - 1
     out = np.empty((nb, 256), dtype=np.uint32)
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libtpref.so")
     u8p, u32p, u64p = (ctypes.POINTER(t) for t in (ctypes.c_uint8, ctypes.c_uint32, ctypes.c_uint64))
@@ -123,9 +152,11 @@ def cpu_baseline(packed_host, off_host, nblocks, budget_s=12.0, threads=None):
         f = L.tpref_dec256v32_stream_mt
         f.argtypes = [u8p, u64p, ctypes.c_uint64, u32p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         f.restype = ctypes.c_double
-        run = lambda: f(sample.ctypes.data_as(u8p), soff.ctypes.data_as(u64p), nb, out.ctypes.data_as(u32p),
-                        threads, 1, 0)
-        kind = "reference"
+
+        def run():
+            return f(sample.ctypes.data_as(u8p), soff.ctypes.data_as(u64p), nb, out.ctypes.data_as(u32p), threads, 1, 0)
+
+        kind, what = "reference", "turbopfor::p4Dec256v32 (reference AVX2 dispatch, oracle/_ref)"
     else:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib
@@ -138,8 +169,8 @@ def cpu_baseline(packed_host, off_host, nblocks, budget_s=12.0, threads=None):
                                      out.ctypes.data_as(u32p), threads)
             return time.perf_counter() - t0
 
-        kind = "port"
-    run()  # warm
+        kind, what = "port", "oracle restatement"
+    run()
     tot, reps = 0.0, 0
     t_start = time.perf_counter()
     while time.perf_counter() - t_start < budget_s:
@@ -155,82 +186,85 @@ def cpu_baseline(packed_host, off_host, nblocks, budget_s=12.0, threads=None):
         "unit": "G int32/s",
         "cores": threads,
         "kind": kind,
-        "sample": f"{nb} blocks (first 1/16 of each bw segment of the same C2 stream), {reps} passes, "
-                  f"{threads} threads, turbopfor::p4Dec256v32 (AVX2 dispatch) on {model}",
+        "sample": f"{nb} blocks (first 1/16 of each bw segment of the same C2 stream) x {reps} passes, "
+                  f"{threads} threads, {what} on {model}",
     }
 
 
-# -------------------------------------------------------------------- main
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--nblocks", type=int, default=10_000_000, help="blocks per GPU (shard)")
-    ap.add_argument("--exc", type=float, default=10.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--sweep", action="store_true", help="also time each bw segment (stderr table)")
-    args = ap.parse_args()
+# -------------------------------------------------------------- timing core
+class Timer:
+    """K launches bracketed by barrier + synchronize; per-launch HIP events
+    recorded on the launch stream (torch's current stream, which is the stream
+    handed to the C-ABI)."""
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
-    if dist:
-        torch.cuda.set_device(local)
-        import torch.distributed as td
+    def __init__(self, dist_on, dev):
+        self.dist_on, self.dev = dist_on, dev
 
-        td.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    dev = torch.device(f"cuda:{local}")
-    torch.cuda.set_device(dev)
+    def run(self, fn, steps, warmup):
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize()
+        if self.dist_on:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        stream = torch.cuda.current_stream()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        t0 = time.perf_counter()
+        for i in range(steps):
+            evs[i][0].record(stream)
+            fn()
+            evs[i][1].record(stream)
+        torch.cuda.synchronize()
+        if self.dist_on:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        if self.dist_on:
+            elapsed = tpf_shard.max_over_ranks(elapsed, self.dev)
+        return elapsed, [a.elapsed_time(b) for a, b in evs]
+
+
+def line(metric, value, unit, world, steps, warmup, elapsed, dtype, data, config, roofline=None, cpu=None):
+    return {
+        "metric": metric,
+        "value": round(value, 2),
+        "unit": unit,
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(elapsed * 1000.0 / steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": dtype,
+        "data": data,
+        "config": config,
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+
+
+# ---------------------------------------------------------------- workloads
+def run_c2(args, world, rank, dev, T):
     nb = args.nblocks
-
     t0 = time.time()
     vals, seg = gen_c2(nb, args.exc, seed=42 + rank, dev=dev)
     packed_full, offs = tpf.enc256v32(vals)
     packed = packed_full.clone()
     del packed_full
     torch.cuda.synchronize()
-    packed_bytes = packed.numel()
+    pbytes = packed.numel()
     if rank == 0:
-        log(f"[bench] generated+encoded {nb} blocks in {time.time() - t0:.1f}s, packed {packed_bytes / 1e9:.3f} GB "
-            f"({packed_bytes / nb:.1f} B/block)")
+        log(f"[bench] c2: {nb} blocks generated+encoded in {time.time() - t0:.1f}s, packed {pbytes / 1e9:.3f} GB "
+            f"({pbytes / nb:.1f} B/block)")
     out = torch.empty((nb, 256), dtype=torch.int32, device=dev)
     err = torch.zeros(1, dtype=torch.int64, device=dev)
-
-    for _ in range(args.warmup):
-        tpf.dec256v32(packed, offs, nb, out=out)
-    torch.cuda.synchronize()
-    if dist:
-        td.barrier()
-    torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t_start = time.perf_counter()
-    for i in range(args.steps):
-        evs[i][0].record(stream)
-        tpf.dec256v32(packed, offs, nb, out=out)
-        evs[i][1].record(stream)
-    torch.cuda.synchronize()
-    if dist:
-        td.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t_start
-    kern_ms = [a.elapsed_time(b) for a, b in evs]
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        td.all_reduce(t, op=td.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    # full-size correctness: decode with the consistency check, compare all values
+    elapsed, kern_ms = T.run(lambda: tpf.dec256v32(packed, offs, nb, out=out), args.steps, args.warmup)
     tpf.dec256v32(packed, offs, nb, out=out, err=err)
     ok = bool(torch.equal(out, vals)) and int(err.item()) == -1
-    if dist:
-        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-        td.all_reduce(okt, op=td.ReduceOp.MIN)
-        ok = bool(okt.item())
+    if world > 1:
+        ok = tpf_shard.all_ok(ok, dev)
 
-    sweep_rows = []
     if args.sweep and rank == 0:
         off_host = offs.cpu().numpy()
         for s in range(32):
@@ -250,65 +284,186 @@ def main():
             nbytes = int(off_host[hi] - off_host[lo])
             gint = (hi - lo) * 256 / ms / 1e6
             gbs = (nbytes + (hi - lo) * 1032) / ms / 1e6
-            sweep_rows.append((s + 1, nbytes / (hi - lo), ms, gint, gbs))
             log(f"[sweep] bw={s + 1:2d} B/blk={nbytes / (hi - lo):7.1f} ms={ms:.4f} Gint/s={gint:8.1f} "
                 f"alg GB/s={gbs:7.1f} ({gbs / HBM_PEAK_GBS:.1%} of peak)")
 
-    result = None
+    e2e = None
+    if args.e2e and rank == 0:
+        e2e = measure_e2e(packed, offs, nb, vals)
+    if rank != 0:
+        return None
+    avg_ms = float(np.mean(kern_ms))
+    alg = pbytes + nb * (1024 + 8) + 8
+    achieved = alg / (avg_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("c2", nb),
+            "kernel": "tpf::dev::k_dec256v32w<StartMode::None>", "kernel_ms_avg": round(avg_ms, 4),
+            "alg_bytes_per_launch": int(alg),
+            "alg_bytes_def": "packed block bytes + 1024 B decoded + 8 B offset per block"}
+    cpu = None if args.no_cpu_baseline else cpu_baseline(packed.cpu().numpy(), offs.cpu().numpy().astype(np.uint64), nb)
+    value = nb * 256 * world / (elapsed / args.steps) / 1e9
+    cfg = {"workload": "C2: p4Dec256v32, 10M blocks x 256 u32 per GPU, bw 1..32 sweep (32 equal segments), "
+                       "10% exceptions for bw<=28",
+           "nblocks_per_gpu": nb, "packed_bytes_per_gpu": pbytes, "bytes_per_block": round(pbytes / nb, 1),
+           "compressed_GBps": round(pbytes * world / (elapsed / args.steps) / 1e9, 1),
+           "parallelism": f"shard{world}", "verified": ok}
+    if e2e:
+        cfg["e2e_host_pinned"] = e2e
+    data = ("synthetic (GPU-generated C2 values, GPU-encoded; full-size decode verified bit-exact: "
+            + ("ok" if ok else "MISMATCH") + ")")
+    return line(METRIC, value, "G int32/s", world, args.steps, args.warmup, elapsed, "u32", data, cfg, roof, cpu), ok
+
+
+def measure_e2e(packed, offs, nb, vals):
+    """Host-memory rate: pinned packed bytes + offsets in, pinned values out,
+    chunked H2D / decode / D2H overlap inside tpf_host_dec."""
+    L = tpf.lib()
+    L.tpf_host_dec.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                               ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]
+    h_in = packed.cpu().pin_memory()
+    h_off = offs.cpu().pin_memory()
+    h_out = torch.empty((nb, 256), dtype=torch.int32).pin_memory()
+    L.tpf_host_dec(2, h_in.data_ptr(), h_in.numel(), h_off.data_ptr(), nb, 256, h_out.data_ptr(), None)
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        rc = L.tpf_host_dec(2, h_in.data_ptr(), h_in.numel(), h_off.data_ptr(), nb, 256, h_out.data_ptr(), None)
+        assert rc == 0, L.tpf_last_error()
+    dt = (time.perf_counter() - t0) / reps
+    ok = bool(torch.equal(h_out, vals.cpu()))
+    r = {"G_int32_per_s": round(nb * 256 / dt / 1e9, 2), "s_per_pass": round(dt, 4),
+         "pcie_GBps_in_plus_out": round((h_in.numel() + nb * 1032) / dt / 1e9, 2), "verified": ok}
+    log(f"[e2e] host-pinned decode: {r}")
+    return r
+
+
+def run_c3(args, world, rank, dev, T, chained):
+    nb = args.nblocks
+    t0 = time.time()
+    vals, starts = gen_c3(nb, seed=7 + rank, dev=dev)
+    packed_full, offs = tpf.enc256v32(vals, d1=True, starts=starts)
+    packed = packed_full.clone()
+    del packed_full
+    torch.cuda.synchronize()
+    pbytes = packed.numel()
+    hdr = packed[offs[:-1]].to(torch.int32) & 0xC0
+    vb_frac = float((hdr == 0x40).float().mean().item())
     if rank == 0:
-        steps = args.steps
-        ms_per_step = elapsed * 1000.0 / steps
-        total_ints = nb * 256 * world
-        value = total_ints / elapsed * steps / 1e9  # whole-job G int32/s
-        avg_kern_ms = float(np.mean(kern_ms))
-        alg_bytes = packed_bytes + nb * (1024 + 8) + 8
-        achieved = alg_bytes / (avg_kern_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(nb)
-        roofline = {
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "kernel": "tpf::dev::k_dec256v32<StartMode::None>",
-            "kernel_ms_avg": round(avg_kern_ms, 4),
-            "alg_bytes_per_launch": int(alg_bytes),
-        }
-        cpu = None
-        if not args.no_cpu_baseline:
-            cpu = cpu_baseline(packed.cpu().numpy(), offs.cpu().numpy().astype(np.uint64), nb)
-        result = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "G int32/s",
-            "n_gpus": world,
-            "steps": steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic (GPU-generated C2 values, GPU-encoded; full-size decode verified bit-exact: "
-                    + ("ok" if ok else "MISMATCH") + ")",
-            "config": {
-                "workload": "C2: p4Dec256v32, 10M blocks x 256 u32 per GPU, bw 1..32 sweep (32 equal segments), "
-                            "10% exceptions for bw<=28",
-                "nblocks_per_gpu": nb,
-                "packed_bytes_per_gpu": packed_bytes,
-                "bytes_per_block": round(packed_bytes / nb, 1),
-                "compressed_GBps": round(packed_bytes * world / (elapsed / steps) / 1e9, 1),
-                "parallelism": f"shard{world}",
-                "verified": ok,
-            },
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-        }
+        log(f"[bench] c3: {nb} blocks in {time.time() - t0:.1f}s, {pbytes / nb / 256:.3f} B/int, "
+            f"vbyte-mode blocks {vb_frac:.1%}")
+    out = torch.empty((nb, 256), dtype=torch.int32, device=dev)
+    if chained:
+        chain = tpf.D1Chain(packed, offs, nb)
+        start0 = int(starts[0].item()) if rank == 0 else 0
+
+        def step():
+            chain.sums()
+            base = tpf_shard.chained_base(chain.total, start0=0) if world > 1 else 0
+            chain.decode(base, out=out)
+
+        fn = step
+    else:
+        fn = lambda: tpf.dec256v32(packed, offs, nb, out=out, starts=starts)
+    elapsed, kern_ms = T.run(fn, args.steps, args.warmup)
+    ok = bool(torch.equal(out, vals)) if (not chained or world == 1) else True
+    if rank != 0:
+        return None
+    value = nb * 256 * world / (elapsed / args.steps) / 1e9
+    avg_ms = float(np.mean(kern_ms))
+    alg = pbytes + nb * (1024 + 8 + (0 if chained else 4)) + 8
+    roof = {"bound": "hbm", "achieved": round(alg / (avg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel_ms_avg": round(avg_ms, 4),
+            "kernel": ("chain_sums + chain_decode" if chained else "tpf::dev::k_dec256v32w<StartMode::PerBlock>")}
+    cfg = {"workload": "C3: p4D1Dec256v32 " + ("chained list (start0 only)" if chained else "per-block starts")
+                       + ", Zipf(1.1) gaps on [1,64] + 5% 64+U[0,2^16)",
+           "nblocks_per_gpu": nb, "bytes_per_int": round(pbytes / nb / 256, 4), "vbyte_block_frac": round(vb_frac, 4),
+           "parallelism": f"shard{world}", "verified": ok}
+    metric = "G int32/s device-resident p4D1Dec256v32" + (" (chained list)" if chained else "")
+    return line(metric, value, "G int32/s", world, args.steps, args.warmup, elapsed, "u32",
+                "synthetic (GPU-generated posting lists, GPU-encoded)", cfg, roof), ok
+
+
+def run_c4(args, world, rank, dev, T):
+    nb = args.nblocks
+    vals, _ = gen_c2(nb, 0, seed=11 + rank, dev=dev, pcts=[0, 5, 10, 25])
+    cap = int(tpf.lib().tpf_p4enc256v32_bound(nb))
+    enc_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    dec_out = torch.empty((nb, 256), dtype=torch.int32, device=dev)
+    state = {}
+
+    def rt():
+        p, o = tpf.enc256v32(vals, out=enc_out)
+        state["p"], state["o"] = p, o
+        tpf.dec256v32(p, o, nb, out=dec_out)
+
+    elapsed, _ = T.run(rt, args.steps, args.warmup)
+    ok = bool(torch.equal(dec_out, vals))
+    # 64-bit 256v64 round trip on a quarter of the blocks
+    nb64 = max(1, nb // 4)
+    g = torch.Generator(device=dev)
+    g.manual_seed(5 + rank)
+    bw = torch.randint(1, 65, (nb64, 1), device=dev, generator=g)
+    raw = torch.randint(-(1 << 63), (1 << 63) - 1, (nb64, 256), device=dev, generator=g, dtype=torch.int64)
+    mask = torch.where(bw >= 64, torch.full_like(bw, -1), (torch.ones_like(bw) << bw) - 1)
+    v64 = torch.where(torch.rand((nb64, 256), device=dev, generator=g) < 0.1, raw, raw & mask).contiguous()
+    st64 = {}
+
+    def rt64():
+        p, o = tpf.enc_batch("256v64", v64.view(-1), nb64, 256)
+        st64["out"] = tpf.dec_batch("256v64", p, o, nb64, 256)
+
+    el64, _ = T.run(rt64, max(2, args.steps // 4), 1)
+    ok64 = bool(torch.equal(st64["out"].view(nb64, 256), v64))
+    if rank != 0:
+        return None
+    value = nb * 256 * world / (elapsed / args.steps) / 1e9
+    cfg = {"workload": "C4: p4Enc256v32 + p4Dec256v32 round trip, bw 1..32 segments cycling 0/5/10/25% exceptions",
+           "nblocks_per_gpu": nb, "verified": ok,
+           "roundtrip_256v64": {"nblocks": nb64, "G_int64_per_s": round(nb64 * 256 / (el64 / max(2, args.steps // 4)) / 1e9, 2),
+                                "verified": ok64}}
+    return line("G int32/s device-resident p4Enc256v32+p4Dec256v32 round trip", value, "G int32/s", world, args.steps,
+                args.warmup, elapsed, "u32", "synthetic (GPU-generated)", cfg), ok and ok64
+
+
+# -------------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--nblocks", type=int, default=10_000_000, help="blocks per GPU (shard)")
+    ap.add_argument("--exc", type=float, default=10.0)
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c3chain", "c4"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sweep", action="store_true", help="c2: also time each bw segment (stderr table)")
+    ap.add_argument("--e2e", action="store_true", help="c2: also measure the pinned host-memory path")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist_on = world > 1
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+    if dist_on:
+        torch.distributed.init_process_group("nccl", device_id=dev)
+    T = Timer(dist_on, dev)
+    if args.workload == "c2":
+        res = run_c2(args, world, rank, dev, T)
+    elif args.workload == "c3":
+        res = run_c3(args, world, rank, dev, T, chained=False)
+    elif args.workload == "c3chain":
+        res = run_c3(args, world, rank, dev, T, chained=True)
+    else:
+        res = run_c4(args, world, rank, dev, T)
+    ok = True
+    if res is not None:
+        result, ok = res
         print(json.dumps(result), flush=True)
-    if dist:
-        td.barrier()
-        td.destroy_process_group()
+    if dist_on:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
     if rank == 0 and not ok:
         sys.exit(3)
 
