@@ -12,6 +12,8 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+
 namespace tpf::dev
 {
 
@@ -125,8 +127,8 @@ __device__ __forceinline__ uint64_t lane_u64(uint64_t v, uint32_t lane)
     return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
-template <StartMode SM>
-__global__ __launch_bounds__(256) void k_dec256v32w(const DecArgs A)
+template <StartMode SM, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
 {
     const uint8_t * in = A.in;
     const uint64_t in_bytes = A.in_bytes;
@@ -188,12 +190,34 @@ namespace tpf
 
 namespace
 {
+// TPF_DEC_MINW selects the occupancy the register allocator targets
+// (launch-bounds minimum waves per SIMD; A/B knob, default measured best).
+int dec_minw()
+{
+    static const int v = [] {
+        const char * e = std::getenv("TPF_DEC_MINW");
+        return e ? std::atoi(e) : 7;
+    }();
+    return v;
+}
+
 template <dev::StartMode SM>
 hipError_t launch_mode(const dev::DecArgs & A, hipStream_t stream)
 {
     const uint64_t per_wg = 4ull * dev::kRun;
     const uint32_t grid = static_cast<uint32_t>((A.nblocks + per_wg - 1) / per_wg);
-    hipLaunchKernelGGL(dev::k_dec256v32w<SM>, dim3(grid), dim3(256), 0, stream, A);
+    switch (dec_minw())
+    {
+        case 8:
+            hipLaunchKernelGGL((dev::k_dec256v32w<SM, 8>), dim3(grid), dim3(256), 0, stream, A);
+            break;
+        case 6:
+            hipLaunchKernelGGL((dev::k_dec256v32w<SM, 1>), dim3(grid), dim3(256), 0, stream, A);
+            break;
+        default:
+            hipLaunchKernelGGL((dev::k_dec256v32w<SM, 7>), dim3(grid), dim3(256), 0, stream, A);
+            break;
+    }
     return hipGetLastError();
 }
 } // namespace
