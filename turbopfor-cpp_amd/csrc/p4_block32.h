@@ -93,24 +93,58 @@ __device__ __forceinline__ BitmapInfo read_bitmap256(const uint32_t * lds, uint3
 __device__ __forceinline__ void patch_bitmap256(const uint32_t * lds, const BitmapInfo & bi, uint32_t xs, uint32_t bx,
                                                 uint32_t b, uint32_t t, u32x4 & v)
 {
+    // Branch-free: with ~10% exceptions every one of the four bit positions is
+    // set in some lane of almost every block, so per-bit `if`s would execute
+    // anyway and only add exec-mask (SALU) work.  A lane without the bit reads
+    // a harmless in-slot word and masks it out.
     const uint32_t u = t >> 4;
     const uint32_t bo = 4u * (t & 15u);
     uint32_t before = (u > 0 ? bi.pc0 : 0u) + (u > 1 ? bi.pc1 : 0u) + (u > 2 ? bi.pc2 : 0u);
     before += __builtin_popcountll(bi.word & ((1ull << bo) - 1ull));
     const uint32_t my = static_cast<uint32_t>(bi.word >> bo) & 0xFu;
-    if (my == 0u)
-        return;
-    const uint32_t xsbit = xs * 8u;
+    const uint32_t bp = xs * 8u + before * bx;
+    const uint32_t r1 = my & 1u, r2 = __builtin_popcount(my & 3u), r3 = __builtin_popcount(my & 7u);
+    const uint32_t e0 = lds_bits(lds, bp, bx), e1 = lds_bits(lds, bp + r1 * bx, bx);
+    const uint32_t e2 = lds_bits(lds, bp + r2 * bx, bx), e3 = lds_bits(lds, bp + r3 * bx, bx);
+    v.x |= (my & 1u) ? shl32(e0, b) : 0u;
+    v.y |= (my & 2u) ? shl32(e1, b) : 0u;
+    v.z |= (my & 4u) ? shl32(e2, b) : 0u;
+    v.w |= (my & 8u) ? shl32(e3, b) : 0u;
+}
+
+// ds_bpermute: value of x in lane `lane` (lane taken mod 64).
+__device__ __forceinline__ uint32_t bperm(uint32_t x, uint32_t lane)
+{
+    return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(lane << 2), static_cast<int>(x)));
+}
+
+// Start positions of consecutive variable-length values inside a 64-byte
+// window, without a serial walk.  nxt = t + len(byte t) is "the next start if
+// t is one"; J_i = nxt applied 2^i times, stopping at the first position
+// >= 64 (binary lifting, 5 ds_bpermute), then lane k composes the J_i of the
+// bits of k starting from sp (6 ds_bpermute).  Returns p_k = position of the
+// k-th value from sp (>= 64: beyond the window, the smallest such = end of the
+// window's last value).
+__device__ __forceinline__ uint32_t window_starts(uint32_t nxt, uint32_t sp, uint32_t t)
+{
+    uint32_t J[6];
+    J[0] = nxt;
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j)
+    for (int i = 1; i < 6; ++i)
     {
-        if ((my >> j) & 1u)
-        {
-            const uint32_t k = before + __builtin_popcount(my & ((1u << j) - 1u));
-            const uint32_t e = lds_bits(lds, xsbit + k * bx, bx);
-            or_comp(v, j, shl32(e, b));
-        }
+        const uint32_t x = J[i - 1];
+        const uint32_t r = bperm(J[i - 1], x);
+        J[i] = x >= 64u ? x : r;
     }
+    uint32_t p = sp;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+    {
+        const uint32_t r = bperm(J[i], p);
+        const uint32_t q = p >= 64u ? p : r;
+        p = ((t >> i) & 1u) ? q : p;
+    }
+    return p;
 }
 
 // vbyte exceptions (p4dec256v32_scalar.cpp:123-136; vbDec32 p4_scalar_internal.cpp:215-237,
@@ -147,44 +181,29 @@ __device__ __forceinline__ uint32_t vbyte_exceptions(const uint32_t * lds, uint3
         vend = v0;
         while (found < xn)
         {
-            const uint32_t by = lds_byte(lds, c + t);
-            const uint32_t len = by < 0x9Cu ? 1u : by < 0xDCu ? 2u : by < 0xFCu ? 3u : by == 0xFCu ? 4u : 5u;
-            const uint64_t L2 = __ballot(len >= 2u), L3 = __ballot(len >= 3u), L4 = __ballot(len >= 4u),
-                           L5 = __ballot(len >= 5u);
-            const uint32_t need = xn - found;
-            uint64_t M = 0;
-            uint32_t cnt = 0;
-            while (sp < 64u && cnt < need)
+            const uint32_t by0 = lds_byte(lds, c + t);
+            const uint32_t len0 = by0 < 0x9Cu ? 1u : by0 < 0xDCu ? 2u : by0 < 0xFCu ? 3u : by0 == 0xFCu ? 4u : 5u;
+            const uint32_t p = window_starts(t + len0, sp, t);
+            const uint32_t m = static_cast<uint32_t>(__builtin_popcountll(__ballot(p < 64u)));
+            const uint32_t cnt = min(m, xn - found);
+            // end of value k (exact, may pass 64).  The permute must run in
+            // every lane: ds_bpermute reads 0 from a lane that is inactive.
+            const uint32_t pn = bperm(t + len0, p);
+            const uint32_t pe = p < 64u ? pn : p;
+            if (t < cnt)
             {
-                M |= 1ull << sp;
-                ++cnt;
-                sp += 1u + static_cast<uint32_t>((L2 >> sp) & 1ull) + static_cast<uint32_t>((L3 >> sp) & 1ull)
-                    + static_cast<uint32_t>((L4 >> sp) & 1ull) + static_cast<uint32_t>((L5 >> sp) & 1ull);
+                const uint32_t by = lds_byte(lds, c + p);
+                const uint32_t d = lds_u32(lds, c + p + 1u);
+                const uint32_t v2 = ((by - 0x9Cu) << 8) + (d & 0xFFu) + 156u;
+                const uint32_t v3 = (d & 0xFFFFu) + ((by - 0xDCu) << 16) + 16540u;
+                const uint32_t val = by < 0x9Cu ? by : by < 0xDCu ? v2 : by < 0xFCu ? v3 : by == 0xFCu ? (d & 0xFFFFFFu) : d;
+                tmp[(found + t) & 255u] = val;
             }
-            if ((M >> t) & 1ull)
-            {
-                const uint32_t k = found + __builtin_popcountll(M & lanemask_lt());
-                const uint32_t d = lds_u32(lds, c + t + 1u);
-                uint32_t val;
-                if (by < 0x9Cu)
-                    val = by;
-                else if (by < 0xDCu)
-                    val = ((by - 0x9Cu) << 8) + (d & 0xFFu) + 156u;
-                else if (by < 0xFCu)
-                    val = (d & 0xFFFFu) + ((by - 0xDCu) << 16) + 16540u;
-                else if (by == 0xFCu)
-                    val = d & 0xFFFFFFu;
-                else
-                    val = d;
-                tmp[k & 255u] = val;
-            }
+            const uint32_t e_last = uni(__builtin_amdgcn_readlane(pe, cnt - 1u));
             found += cnt;
-            vend = c + sp;
-            if (sp >= 64u)
-            {
-                sp -= 64u;
-                c += 64u;
-            }
+            vend = c + e_last;
+            sp = e_last >= 64u ? e_last - 64u : e_last;
+            c += e_last >= 64u ? 64u : 0u;
         }
         wave_lds_sync();
         for (uint32_t k = t; k < xn; k += kWave)

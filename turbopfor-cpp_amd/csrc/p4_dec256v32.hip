@@ -39,129 +39,122 @@ struct DecArgs
 };
 
 // ---------------------------------------------------------------------------
-// Wave-independent variant: every wave owns a private LDS slot and walks
-// blocks wg, wg+W, wg+2W (W = all waves of the grid) with a software
-// pipeline: while block k is decoded, the bytes of block k+1 are already in
-// flight (two unconditional 16-byte buffer loads per lane = 2 KB per wave) and
-// the offsets of block k+2 are prefetched through the scalar cache.  The loop
-// is unrolled by two with separate register sets (A/B) so no in-flight load
-// result is ever copied (a copy would force s_waitcnt vmcnt(0) at the loop
-// head).  No workgroup barriers at all.
+// Wave-independent kernel: every wave owns a private LDS slot and decodes a
+// contiguous run of kRun blocks with a software pipeline: while block j is
+// decoded, the bytes of blocks j+1 and j+2 are in flight (two unconditional
+// 16-byte buffer loads per lane = up to 2 KB per block).  Three register
+// chunks rotate (loop unrolled by three) so no in-flight load result is ever
+// copied (a copy forces s_waitcnt vmcnt(0)).  No workgroup barriers at all.
+//
+// Control plane in vector lanes: the run's offsets arrive with one vector load
+// (lane j = block first+j) and every per-block quantity the loop needs (chunk
+// base, span, byte offset inside the chunk, expected length, start value) is
+// computed once per run in VALU and fetched per block with v_readlane.  The
+// scalar unit is shared by the CU's four SIMDs; per-block 64-bit address
+// arithmetic on it was the measured limiter.
 constexpr uint32_t kSlotBytes = 2304 + 64;
+constexpr uint32_t kRun = 16; // blocks per wave (must stay <= 62: lanes >= n hold "no block")
+
+// ctl word bits
+constexpr uint32_t kCtlSpan = 0xFFFu;    // bytes the fast path stages (0: none)
+constexpr uint32_t kCtlShift = 12;       // [12,16): block start inside its 16-aligned chunk
+constexpr uint32_t kCtlSlow = 1u << 16;  // > 2 KB or straddles the stream end: guarded loads
+constexpr uint32_t kCtlTwo = 1u << 17;   // second 1 KB half present
 
 struct Chunk
 {
-    u32x4 a, b;    // bytes [0,1024) and [1024,2048) of the 16-aligned block image
-    uint64_t base; // 16-aligned absolute start
-    uint32_t span; // bytes to stage from base
-    uint32_t avail;
+    u32x4 a, b; // bytes [0,1024) and [1024,2048) of the 16-aligned block image
 };
 
-// Always issues exactly two loads (a block that does not exist gets an empty
-// descriptor: the loads return zeros without touching memory) so every path
-// through the pipelined loop has the same vmcnt pattern and the compiler can
-// wait with vmcnt(N > 0) instead of draining.
-__device__ __forceinline__ void issue_chunk(Chunk & c, uint64_t in_base, uint64_t in_end, uint64_t o, uint64_t e, bool valid,
-                                            uint32_t t)
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane)
 {
-    c.base = (in_base + o) & ~15ull;
-    c.span = static_cast<uint32_t>(min_u64(sub_sat(in_base + e, c.base), kSlotBytes - 64));
-    c.avail = valid ? static_cast<uint32_t>(min_u64(sub_sat(in_end, c.base), kSlotBytes)) : 0u;
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(c.base), c.avail);
-    // lanes past the block get an out-of-range offset: no memory traffic, zeros
-    const uint32_t oa = 16u * t < c.span ? 16u * t : 0x80000000u;
-    const uint32_t ob = 1024u + 16u * t < c.span ? 1024u + 16u * t : 0x80000000u;
-    c.a = buf_load16(rs, oa);
-    c.b = buf_load16(rs, ob);
-}
-
-template <StartMode SM>
-__device__ __forceinline__ bool consume_chunk(const Chunk & c, uint64_t in_base, uint64_t o, uint64_t e, uint64_t blk,
-                                              uint32_t * slot, uint32_t * scr, const DecArgs & A, uint32_t t)
-{
-    reinterpret_cast<u32x4 *>(slot)[t] = c.a;
-    if (c.span > 1024u)
-        reinterpret_cast<u32x4 *>(slot)[64 + t] = c.b;
-    if (c.span > 2048u || c.span + 16u > c.avail)
-    {
-        // rare: > 2 KB blocks (third chunk) or the chunk straddling the end of
-        // the stream (a raw buffer load that crosses num_records returns 0)
-        const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(c.base), c.avail);
-        const uint8_t * bp = reinterpret_cast<const uint8_t *>(c.base);
-        for (uint32_t x = 16u * t; x < c.span; x += 1024u)
-            reinterpret_cast<u32x4 *>(slot)[x >> 4] = load16_guarded(bp, rs, x, c.avail);
-    }
-    wave_lds_sync();
-    u32x4 v;
-    const uint32_t used = decode_block256v32(slot, static_cast<uint32_t>(in_base + o - c.base), scr, t, v);
-    if constexpr (SM == StartMode::SumOnly)
-    {
-        const uint32_t s = wave_sum(v.x + v.y + v.z + v.w + 4u);
-        if (t == 0)
-            A.sums[blk] = s;
-    }
-    else
-    {
-        if constexpr (SM == StartMode::PerBlock)
-            apply_delta1_256(v, A.starts[blk]);
-        if constexpr (SM == StartMode::Prefix)
-            apply_delta1_256(v, A.base + (blk ? A.starts[blk - 1] : 0u));
-        reinterpret_cast<u32x4 *>(A.out + blk * 256u)[t] = v;
-    }
-    wave_lds_sync();
-    return static_cast<uint64_t>(used) == e - o;
-}
-
-// Each wave decodes a contiguous run of kRun blocks [first, first+kRun): the
-// run's kRun+1 offsets arrive with one vector load (lane i holds off[first+i])
-// and are broadcast with v_readlane, so the per-block control path issues no
-// memory instruction besides the pipelined data loads.  The grid is NOT
-// persistent: ~nblocks/(4*kRun) workgroups let the dispatcher balance the CUs
-// (a persistent grid larger than the resident set leaves a tail wave).
-constexpr uint32_t kRun = 16;
-
-__device__ __forceinline__ uint64_t lane_u64(uint64_t v, uint32_t lane)
-{
-    const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), lane);
-    const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), lane);
-    return (static_cast<uint64_t>(hi) << 32) | lo;
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(lane)));
 }
 
 template <StartMode SM, int MINW>
 __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
 {
-    const uint8_t * in = A.in;
-    const uint64_t in_bytes = A.in_bytes;
-    const uint64_t * off = A.off;
-    const uint64_t nblocks = A.nblocks;
     __shared__ uint32_t slots[4][kSlotBytes / 4];
     __shared__ uint32_t scratch[4][kWaveScratchU32];
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
     uint32_t * slot = slots[wv];
     uint32_t * scr = scratch[wv];
-    const uint64_t in_base = reinterpret_cast<uint64_t>(in);
-    const uint64_t in_end = in_base + in_bytes;
+    const uint64_t in_base = reinterpret_cast<uint64_t>(A.in);
+    const uint64_t in_end = in_base + A.in_bytes;
 
     const uint64_t first = (static_cast<uint64_t>(blockIdx.x) * 4u + wv) * kRun;
-    if (first >= nblocks)
+    if (first >= A.nblocks)
         return;
-    const uint32_t n = static_cast<uint32_t>(min_u64(kRun, nblocks - first));
-    const uint64_t offv = t <= n ? off[first + t] : 0ull;
-    uint64_t bad = ~0ull;
+    const uint32_t n = static_cast<uint32_t>(min_u64(kRun, A.nblocks - first));
 
-    // Three register chunks rotate (unrolled by three, no copies): while block
-    // j is decoded, blocks j+1 and j+2 are in flight.
-    Chunk C0, C1, C2;
+    // ---- per-run control plane, lane j = block first+j ---------------------
+    const bool valid = t < n;
+    const uint64_t o = valid ? A.off[first + t] : 0ull;
+    const uint64_t e = valid ? A.off[first + t + 1u] : 0ull;
+    const uint64_t ab = in_base + o;
+    const uint64_t cb = ab & ~15ull;
+    const uint32_t span = valid ? static_cast<uint32_t>(min_u64(sub_sat(in_base + e, cb), kSlotBytes - 64)) : 0u;
+    const uint32_t avail = valid ? static_cast<uint32_t>(min_u64(sub_sat(in_end, cb), kSlotBytes)) : 0u;
+    const bool slow = valid && (span > 2048u || span + 16u > avail);
+    const uint32_t ctlv = (slow ? 0u : span) | ((static_cast<uint32_t>(ab) & 15u) << kCtlShift) | (slow ? kCtlSlow : 0u)
+        | (!slow && span > 1024u ? kCtlTwo : 0u);
+    const uint32_t lenv = (e >= o && e - o < 0x10000ull) ? static_cast<uint32_t>(e - o) : 0xFFFFFFFFu;
+    const uint32_t cblo = static_cast<uint32_t>(cb), cbhi = static_cast<uint32_t>(cb >> 32);
+    uint32_t startv = 0u;
+    if constexpr (SM == StartMode::PerBlock)
+        startv = valid ? A.starts[first + t] : 0u;
+    if constexpr (SM == StartMode::Prefix)
+        startv = A.base + ((valid && first + t > 0) ? A.starts[first + t - 1u] : 0u);
+    uint32_t sumv = 0u;
+    uint32_t * const out_run = SM == StartMode::SumOnly ? nullptr : A.out + first * 256u;
+    uint32_t badmask = 0u;
+
     auto issue = [&](Chunk & c, uint32_t jj) {
-        const uint32_t q = min(jj, n - 1);
-        issue_chunk(c, in_base, in_end, lane_u64(offv, q), lane_u64(offv, q + 1), jj < n, t);
+        // jj <= n + 1 <= 63: lanes >= n have ctl 0 (no bytes, no traffic)
+        const uint32_t ctl = rl(ctlv, jj);
+        const uint64_t base = (static_cast<uint64_t>(rl(cbhi, jj)) << 32) | rl(cblo, jj);
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(base), kSlotBytes);
+        const uint32_t fspan = ctl & kCtlSpan;
+        c.a = buf_load16(rs, 16u * t < fspan ? 16u * t : 0x80000000u);
+        c.b = buf_load16(rs, 1024u + 16u * t < fspan ? 1024u + 16u * t : 0x80000000u);
     };
     auto consume = [&](const Chunk & c, uint32_t jj) {
-        const uint64_t o = lane_u64(offv, jj), e = lane_u64(offv, jj + 1);
-        if (!consume_chunk<SM>(c, in_base, o, e, first + jj, slot, scr, A, t))
-            bad = min_u64(bad, first + jj);
+        const uint32_t ctl = rl(ctlv, jj);
+        reinterpret_cast<u32x4 *>(slot)[t] = c.a;
+        if (ctl & kCtlTwo)
+            reinterpret_cast<u32x4 *>(slot)[64 + t] = c.b;
+        if (ctl & kCtlSlow)
+        {
+            // rare: > 2 KB blocks or the chunk straddling the end of the stream
+            // (a raw buffer load that crosses num_records returns 0)
+            const uint32_t sp = rl(span, jj), av = rl(avail, jj);
+            const uint64_t base = (static_cast<uint64_t>(rl(cbhi, jj)) << 32) | rl(cblo, jj);
+            const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(base), av);
+            const uint8_t * bp = reinterpret_cast<const uint8_t *>(base);
+            for (uint32_t x = 16u * t; x < sp; x += 1024u)
+                reinterpret_cast<u32x4 *>(slot)[x >> 4] = load16_guarded(bp, rs, x, av);
+        }
+        wave_lds_sync();
+        u32x4 v;
+        const uint32_t used = decode_block256v32(slot, (ctl >> kCtlShift) & 15u, scr, t, v);
+        if constexpr (SM == StartMode::SumOnly)
+        {
+            const uint32_t s = wave_sum(v.x + v.y + v.z + v.w + 4u);
+            sumv = t == jj ? s : sumv;
+        }
+        else
+        {
+            if constexpr (SM == StartMode::PerBlock || SM == StartMode::Prefix)
+                apply_delta1_256(v, rl(startv, jj));
+            reinterpret_cast<u32x4 *>(out_run + jj * 256u)[t] = v;
+        }
+        wave_lds_sync();
+        if (used != rl(lenv, jj))
+            badmask |= 1u << jj;
     };
+
+    Chunk C0, C1, C2;
     issue(C0, 0);
     issue(C1, 1);
     for (uint32_t j = 0;; j += 3)
@@ -179,8 +172,13 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
         if (j + 3 >= n)
             break;
     }
-    if (A.err != nullptr && t == 0 && bad != ~0ull)
-        atomicMin(A.err, static_cast<unsigned long long>(bad));
+    if constexpr (SM == StartMode::SumOnly)
+    {
+        if (valid)
+            A.sums[first + t] = sumv;
+    }
+    if (A.err != nullptr && t == 0 && badmask != 0u)
+        atomicMin(A.err, static_cast<unsigned long long>(first + __builtin_ctz(badmask)));
 }
 
 } // namespace tpf::dev
