@@ -290,16 +290,22 @@ def run_c2(args, world, rank, dev, T):
     e2e = None
     if args.e2e and rank == 0:
         e2e = measure_e2e(packed, offs, nb, vals)
+    # data-movement ceiling of the same access pattern (same kernel, loads
+    # and stores only, no decode) -- outside the timed region
+    _, probe_ms = T.run(lambda: tpf.probe256v32(packed, offs, nb, out), 10, 2)
     if rank != 0:
         return None
     avg_ms = float(np.mean(kern_ms))
     alg = pbytes + nb * (1024 + 8) + 8
     achieved = alg / (avg_ms * 1e-3) / 1e9
+    probe = alg / (float(np.mean(probe_ms)) * 1e-3) / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("c2", nb),
             "kernel": "tpf::dev::k_dec256v32w<StartMode::None>", "kernel_ms_avg": round(avg_ms, 4),
             "alg_bytes_per_launch": int(alg),
-            "alg_bytes_def": "packed block bytes + 1024 B decoded + 8 B offset per block"}
+            "alg_bytes_def": "packed block bytes + 1024 B decoded + 8 B offset per block",
+            "probe_GBps": round(probe, 1), "frac_of_probe": round(achieved / probe, 4),
+            "probe_def": "tpf_probe256v32: the decode kernel's own loads and stores with decoding removed"}
     cpu = None if args.no_cpu_baseline else cpu_baseline(packed.cpu().numpy(), offs.cpu().numpy().astype(np.uint64), nb)
     value = nb * 256 * world / (elapsed / args.steps) / 1e9
     cfg = {"workload": "C2: p4Dec256v32, 10M blocks x 256 u32 per GPU, bw 1..32 sweep (32 equal segments), "

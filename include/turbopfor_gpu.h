@@ -46,6 +46,13 @@ int tpf_device_count(void);
 int tpf_p4dec256v32_batch(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks,
                           uint32_t *d_out, uint64_t *d_err, void *stream);
 
+/* Measurement only (no reference counterpart): the decode kernel's exact load
+ * and store pattern with the decoding removed -- block i's staged bytes are
+ * written to d_out[256*i..] unchanged.  Gives the data-movement ceiling the
+ * decoder is compared against in bench.py. */
+int tpf_probe256v32(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks,
+                    uint32_t *d_out, void *stream);
+
 /* Replaces turbopfor::p4D1Dec256v32 (include/turbopfor.h:42, dispatch.cpp:97-104):
  * block i is decoded with start d_starts[i] (the value preceding the block). */
 int tpf_p4d1dec256v32_batch(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks,

@@ -94,6 +94,17 @@ int tpf_p4dec256v32_batch(const uint8_t * d_in, uint64_t in_bytes, const uint64_
     return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_p4dec256v32_batch");
 }
 
+int tpf_probe256v32(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nblocks, uint32_t * d_out,
+                    void * stream)
+{
+    if (int rc = check_device())
+        return rc;
+    if (nblocks && (!d_in || !d_off || !d_out))
+        return fail(TPF_EINVAL, "tpf_probe256v32: null pointer");
+    hipError_t e = tpf::launch_probe256v32(d_in, in_bytes, d_off, nblocks, d_out, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_probe256v32");
+}
+
 int tpf_p4d1dec256v32_batch(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nblocks, uint32_t * d_out,
                             const uint32_t * d_starts, uint64_t * d_err, void * stream)
 {

@@ -62,31 +62,27 @@ __device__ __forceinline__ void or_comp(u32x4 & v, uint32_t j, uint32_t x)
 // Bitmap-patch exceptions (p4Dec256PayloadBitmap, p4dec256v32_scalar.cpp:10-66):
 // 32-byte bitmap at bm_pos, then the xn exception high parts as ONE horizontal
 // LSB-first bx-bit stream (bitunpack32Scalar), then the base payload.  Lane t
-// ranks its own bitmap bits with popcounts instead of the serial ctz loop.
-// Returns the payload byte position; *xn_out = exception count.
+// owns values 4t..4t+3, i.e. bits 4(t&7)..4(t&7)+3 of bitmap dword t>>3: it
+// reads that one dword, and its rank among the exceptions is the popcount of
+// the dwords before (one wave scan) plus the bits below its own.  This
+// replaces the serial ctz loop of the reference.
 struct BitmapInfo
 {
-    uint32_t pc0, pc1, pc2, pc3;
-    uint64_t word; // bitmap word holding this lane's 4 bits
+    uint32_t my;     // this lane's 4 bitmap bits
+    uint32_t before; // exceptions at positions < 4t
+    uint32_t xn;     // total (wave-uniform)
 };
 
 __device__ __forceinline__ BitmapInfo read_bitmap256(const uint32_t * lds, uint32_t bm_pos, uint32_t t)
 {
     BitmapInfo bi;
-    uint32_t w[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-        w[i] = lds_u32(lds, bm_pos + 4u * i);
-    uint64_t b0 = (uint64_t(w[1]) << 32) | w[0];
-    uint64_t b1 = (uint64_t(w[3]) << 32) | w[2];
-    uint64_t b2 = (uint64_t(w[5]) << 32) | w[4];
-    uint64_t b3 = (uint64_t(w[7]) << 32) | w[6];
-    bi.pc0 = __builtin_popcountll(b0);
-    bi.pc1 = __builtin_popcountll(b1);
-    bi.pc2 = __builtin_popcountll(b2);
-    bi.pc3 = __builtin_popcountll(b3);
-    const uint32_t u = t >> 4;
-    bi.word = u == 0 ? b0 : u == 1 ? b1 : u == 2 ? b2 : b3;
+    const uint32_t w = lds_u32(lds, bm_pos + 4u * (t >> 3));
+    const uint32_t sh = 4u * (t & 7u);
+    bi.my = (w >> sh) & 0xFu;
+    const uint32_t pcd = __builtin_popcount(w);
+    const uint32_t incl = wave_incl_scan((t & 7u) == 0u ? pcd : 0u);
+    bi.before = incl - pcd + __builtin_popcount(w & ((1u << sh) - 1u));
+    bi.xn = uni(__builtin_amdgcn_readlane(incl, 63));
     return bi;
 }
 
@@ -97,12 +93,8 @@ __device__ __forceinline__ void patch_bitmap256(const uint32_t * lds, const Bitm
     // set in some lane of almost every block, so per-bit `if`s would execute
     // anyway and only add exec-mask (SALU) work.  A lane without the bit reads
     // a harmless in-slot word and masks it out.
-    const uint32_t u = t >> 4;
-    const uint32_t bo = 4u * (t & 15u);
-    uint32_t before = (u > 0 ? bi.pc0 : 0u) + (u > 1 ? bi.pc1 : 0u) + (u > 2 ? bi.pc2 : 0u);
-    before += __builtin_popcountll(bi.word & ((1ull << bo) - 1ull));
-    const uint32_t my = static_cast<uint32_t>(bi.word >> bo) & 0xFu;
-    const uint32_t bp = xs * 8u + before * bx;
+    const uint32_t my = bi.my;
+    const uint32_t bp = xs * 8u + bi.before * bx;
     const uint32_t r1 = my & 1u, r2 = __builtin_popcount(my & 3u), r3 = __builtin_popcount(my & 7u);
     const uint32_t e0 = lds_bits(lds, bp, bx), e1 = lds_bits(lds, bp + r1 * bx, bx);
     const uint32_t e2 = lds_bits(lds, bp + r2 * bx, bx), e3 = lds_bits(lds, bp + r3 * bx, bx);
@@ -217,9 +209,11 @@ __device__ __forceinline__ uint32_t vbyte_exceptions(const uint32_t * lds, uint3
 }
 
 // Decode one 256v32 block at LDS byte s.  Returns consumed bytes (uniform).
+// The header byte and the byte after it (bx / xn) arrive with one read.
 __device__ __forceinline__ uint32_t decode_block256v32(const uint32_t * lds, uint32_t s, uint32_t * scr, uint32_t t, u32x4 & v)
 {
-    const uint32_t h = uni(lds_byte(lds, s));
+    const uint32_t hw = uni(lds_u32(lds, s));
+    const uint32_t h = hw & 0xFFu, x1 = (hw >> 8) & 0xFFu;
     if ((h & 0xC0u) == 0xC0u)
     {
         const uint32_t b = h & 0x3Fu;
@@ -232,7 +226,7 @@ __device__ __forceinline__ uint32_t decode_block256v32(const uint32_t * lds, uin
     if ((h & 0x40u) == 0u)
     {
         const uint32_t hdr = (h & 0x80u) ? 2u : 1u;
-        const uint32_t bx = (h & 0x80u) ? min(uni(lds_byte(lds, s + 1u)), 32u) : 0u;
+        const uint32_t bx = (h & 0x80u) ? min(x1, 32u) : 0u;
         const uint32_t b = min(h & 0x7Fu, 32u);
         if (bx == 0u)
         {
@@ -240,15 +234,14 @@ __device__ __forceinline__ uint32_t decode_block256v32(const uint32_t * lds, uin
             return hdr + 32u * b;
         }
         const BitmapInfo bi = read_bitmap256(lds, s + 2u, t);
-        const uint32_t xn = bi.pc0 + bi.pc1 + bi.pc2 + bi.pc3;
         const uint32_t xs = s + 34u;
-        const uint32_t xbytes = (xn * bx + 7u) >> 3;
+        const uint32_t xbytes = (bi.xn * bx + 7u) >> 3;
         v = unpack256v32_lane(lds, xs + xbytes, b, t);
         patch_bitmap256(lds, bi, xs, bx, b, t, v);
         return 34u + xbytes + 32u * b;
     }
     const uint32_t b = min(h & 0x3Fu, 32u);
-    const uint32_t xn = uni(lds_byte(lds, s + 1u));
+    const uint32_t xn = x1;
     v = unpack256v32_lane(lds, s + 2u, b, t);
     const uint32_t end = vbyte_exceptions(lds, s + 2u + 32u * b, xn, scr, t);
     const u32x4 ex = reinterpret_cast<const u32x4 *>(scr)[t];

@@ -23,6 +23,7 @@ enum class StartMode : int
     PerBlock = 1, // p4D1Dec256v32, start of block i = starts[i]
     Prefix = 2,   // chained list: start of block i = base + incl[i-1] (incl = prefix of block sums)
     SumOnly = 3,  // no output: sums[i] = sum over the block of (v + 1) mod 2^32
+    Probe = 4,    // measurement only: same loads and stores, no decode (data-movement ceiling)
 };
 
 struct DecArgs
@@ -53,7 +54,7 @@ struct DecArgs
 // scalar unit is shared by the CU's four SIMDs; per-block 64-bit address
 // arithmetic on it was the measured limiter.
 constexpr uint32_t kSlotBytes = 2304 + 64;
-constexpr uint32_t kRun = 16; // blocks per wave (must stay <= 62: lanes >= n hold "no block")
+constexpr uint32_t kRunDefault = 16; // blocks per wave (<= 62: lanes >= n hold "no block")
 
 // ctl word bits
 constexpr uint32_t kCtlSpan = 0xFFFu;    // bytes the fast path stages (0: none)
@@ -71,8 +72,25 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane)
     return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(lane)));
 }
 
-template <StartMode SM, int MINW>
-__global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
+// POL (A/B knob): bit 0 = non-temporal loads (measured -4%), bit 1 =
+// non-temporal stores (measured +2.5%, default), bit 2 = block order.
+template <uint32_t POL>
+__device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    return __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), 0, (POL & 1u) ? 2 : 0);
+}
+
+template <uint32_t POL>
+__device__ __forceinline__ void st16(u32x4 * p, const u32x4 & v)
+{
+    if constexpr ((POL & 2u) != 0u)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+template <StartMode SM, uint32_t kRun, uint32_t POL = 0>
+__global__ __launch_bounds__(256, 7) void k_dec256v32w(const DecArgs A)
 {
     __shared__ uint32_t slots[4][kSlotBytes / 4];
     __shared__ uint32_t scratch[4][kWaveScratchU32];
@@ -83,15 +101,20 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
     const uint64_t in_base = reinterpret_cast<uint64_t>(A.in);
     const uint64_t in_end = in_base + A.in_bytes;
 
-    const uint64_t first = (static_cast<uint64_t>(blockIdx.x) * 4u + wv) * kRun;
+    // POL bit 2: the workgroup's 4*kRun blocks are dealt to its waves
+    // round-robin (block first + stride*j) instead of in contiguous runs.
+    constexpr uint32_t stride = (POL & 4u) ? 4u : 1u;
+    const uint64_t first = (POL & 4u) ? static_cast<uint64_t>(blockIdx.x) * 4u * kRun + wv
+                                      : (static_cast<uint64_t>(blockIdx.x) * 4u + wv) * kRun;
     if (first >= A.nblocks)
         return;
-    const uint32_t n = static_cast<uint32_t>(min_u64(kRun, A.nblocks - first));
+    const uint32_t n = static_cast<uint32_t>(min_u64(kRun, (A.nblocks - first + stride - 1u) / stride));
 
     // ---- per-run control plane, lane j = block first+j ---------------------
     const bool valid = t < n;
-    const uint64_t o = valid ? A.off[first + t] : 0ull;
-    const uint64_t e = valid ? A.off[first + t + 1u] : 0ull;
+    const uint64_t blk = first + stride * t;
+    const uint64_t o = valid ? A.off[blk] : 0ull;
+    const uint64_t e = valid ? A.off[blk + 1u] : 0ull;
     const uint64_t ab = in_base + o;
     const uint64_t cb = ab & ~15ull;
     const uint32_t span = valid ? static_cast<uint32_t>(min_u64(sub_sat(in_base + e, cb), kSlotBytes - 64)) : 0u;
@@ -103,12 +126,12 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
     const uint32_t cblo = static_cast<uint32_t>(cb), cbhi = static_cast<uint32_t>(cb >> 32);
     uint32_t startv = 0u;
     if constexpr (SM == StartMode::PerBlock)
-        startv = valid ? A.starts[first + t] : 0u;
+        startv = valid ? A.starts[blk] : 0u;
     if constexpr (SM == StartMode::Prefix)
-        startv = A.base + ((valid && first + t > 0) ? A.starts[first + t - 1u] : 0u);
+        startv = A.base + ((valid && blk > 0) ? A.starts[blk - 1u] : 0u);
     uint32_t sumv = 0u;
     uint32_t * const out_run = SM == StartMode::SumOnly ? nullptr : A.out + first * 256u;
-    uint32_t badmask = 0u;
+    uint64_t badmask = 0u;
 
     auto issue = [&](Chunk & c, uint32_t jj) {
         // jj <= n + 1 <= 63: lanes >= n have ctl 0 (no bytes, no traffic)
@@ -116,11 +139,16 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
         const uint64_t base = (static_cast<uint64_t>(rl(cbhi, jj)) << 32) | rl(cblo, jj);
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(base), kSlotBytes);
         const uint32_t fspan = ctl & kCtlSpan;
-        c.a = buf_load16(rs, 16u * t < fspan ? 16u * t : 0x80000000u);
-        c.b = buf_load16(rs, 1024u + 16u * t < fspan ? 1024u + 16u * t : 0x80000000u);
+        c.a = ld16<POL>(rs, 16u * t < fspan ? 16u * t : 0x80000000u);
+        c.b = ld16<POL>(rs, 1024u + 16u * t < fspan ? 1024u + 16u * t : 0x80000000u);
     };
     auto consume = [&](const Chunk & c, uint32_t jj) {
         const uint32_t ctl = rl(ctlv, jj);
+        if constexpr (SM == StartMode::Probe)
+        {
+            st16<POL>(reinterpret_cast<u32x4 *>(out_run + jj * stride * 256u) + t, c.a | c.b);
+            return;
+        }
         reinterpret_cast<u32x4 *>(slot)[t] = c.a;
         if (ctl & kCtlTwo)
             reinterpret_cast<u32x4 *>(slot)[64 + t] = c.b;
@@ -147,11 +175,11 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
         {
             if constexpr (SM == StartMode::PerBlock || SM == StartMode::Prefix)
                 apply_delta1_256(v, rl(startv, jj));
-            reinterpret_cast<u32x4 *>(out_run + jj * 256u)[t] = v;
+            st16<POL>(reinterpret_cast<u32x4 *>(out_run + jj * stride * 256u) + t, v);
         }
         wave_lds_sync();
         if (used != rl(lenv, jj))
-            badmask |= 1u << jj;
+            badmask |= 1ull << jj;
     };
 
     Chunk C0, C1, C2;
@@ -175,10 +203,10 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
     if constexpr (SM == StartMode::SumOnly)
     {
         if (valid)
-            A.sums[first + t] = sumv;
+            A.sums[blk] = sumv;
     }
     if (A.err != nullptr && t == 0 && badmask != 0u)
-        atomicMin(A.err, static_cast<unsigned long long>(first + __builtin_ctz(badmask)));
+        atomicMin(A.err, static_cast<unsigned long long>(first + stride * __builtin_ctzll(badmask)));
 }
 
 } // namespace tpf::dev
@@ -188,37 +216,68 @@ namespace tpf
 
 namespace
 {
-// TPF_DEC_MINW selects the occupancy the register allocator targets
-// (launch-bounds minimum waves per SIMD; A/B knob, default measured best).
-int dec_minw()
+// A/B knobs (defaults = measured best): TPF_DEC_RUN blocks per wave run,
+// TPF_DEC_POL cache policy bits (see ld16/st16).
+uint32_t env_knob(const char * name, uint32_t dflt)
 {
-    static const int v = [] {
-        const char * e = std::getenv("TPF_DEC_MINW");
-        return e ? std::atoi(e) : 7;
-    }();
+    const char * e = std::getenv(name);
+    return e ? static_cast<uint32_t>(std::atoi(e)) : dflt;
+}
+
+uint32_t dec_run()
+{
+    static const uint32_t v = env_knob("TPF_DEC_RUN", dev::kRunDefault) == 8 ? 8u : 16u;
     return v;
+}
+
+uint32_t dec_pol()
+{
+    static const uint32_t v = env_knob("TPF_DEC_POL", 2u) & 7u;
+    return v;
+}
+
+template <dev::StartMode SM, uint32_t RUN, uint32_t POL>
+hipError_t launch_run(const dev::DecArgs & A, hipStream_t stream)
+{
+    const uint64_t per_wg = 4ull * RUN;  // both block orders cover 4*RUN blocks per workgroup
+    const uint32_t grid = static_cast<uint32_t>((A.nblocks + per_wg - 1) / per_wg);
+    hipLaunchKernelGGL((dev::k_dec256v32w<SM, RUN, POL>), dim3(grid), dim3(256), 0, stream, A);
+    return hipGetLastError();
+}
+
+template <dev::StartMode SM, uint32_t POL>
+hipError_t launch_pol(const dev::DecArgs & A, hipStream_t stream)
+{
+    return dec_run() == 8 ? launch_run<SM, 8, POL>(A, stream) : launch_run<SM, 16, POL>(A, stream);
 }
 
 template <dev::StartMode SM>
 hipError_t launch_mode(const dev::DecArgs & A, hipStream_t stream)
 {
-    const uint64_t per_wg = 4ull * dev::kRun;
-    const uint32_t grid = static_cast<uint32_t>((A.nblocks + per_wg - 1) / per_wg);
-    switch (dec_minw())
+    switch (dec_pol())
     {
-        case 8:
-            hipLaunchKernelGGL((dev::k_dec256v32w<SM, 8>), dim3(grid), dim3(256), 0, stream, A);
-            break;
+        case 1:
+            return launch_pol<SM, 1>(A, stream);
+        case 0:
+            return launch_pol<SM, 0>(A, stream);
+        case 3:
+            return launch_pol<SM, 3>(A, stream);
         case 6:
-            hipLaunchKernelGGL((dev::k_dec256v32w<SM, 1>), dim3(grid), dim3(256), 0, stream, A);
-            break;
+            return launch_pol<SM, 6>(A, stream);
         default:
-            hipLaunchKernelGGL((dev::k_dec256v32w<SM, 7>), dim3(grid), dim3(256), 0, stream, A);
-            break;
+            return launch_pol<SM, 2>(A, stream);
     }
-    return hipGetLastError();
 }
 } // namespace
+
+hipError_t launch_probe256v32(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * out,
+                              hipStream_t stream)
+{
+    if (nblocks == 0)
+        return hipSuccess;
+    const dev::DecArgs A{in, in_bytes, off, nblocks, out, nullptr, 0u, nullptr, nullptr};
+    return launch_mode<dev::StartMode::Probe>(A, stream);
+}
 
 hipError_t launch_dec256v32(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * out,
                             const uint32_t * starts, unsigned long long * err, hipStream_t stream)

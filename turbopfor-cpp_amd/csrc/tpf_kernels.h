@@ -33,6 +33,9 @@ hipError_t launch_enc_generic(int fmt, const void * in, uint64_t nblocks, uint32
 hipError_t launch_dec256v32(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * out,
                             const uint32_t * starts, unsigned long long * err, hipStream_t stream);
 
+hipError_t launch_probe256v32(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * out,
+                              hipStream_t stream);
+
 size_t d1chain_workspace(uint64_t nblocks);
 hipError_t launch_d1chain_sums(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * incl,
                                void * ws, size_t ws_bytes, unsigned long long * err, hipStream_t stream);

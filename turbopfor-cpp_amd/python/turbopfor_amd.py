@@ -45,6 +45,7 @@ def lib():
         L.tpf_device_count.restype = ctypes.c_int
         L.tpf_p4dec256v32_batch.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp, c_vp]
         L.tpf_p4d1dec256v32_batch.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp, c_vp, c_vp]
+        L.tpf_probe256v32.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp]
         L.tpf_p4enc256v32_bound.argtypes = [c_u64]
         L.tpf_p4enc256v32_bound.restype = c_u64
         L.tpf_p4enc256v32_workspace_size.argtypes = [c_u64]
@@ -67,7 +68,7 @@ def lib():
         L.tpf_p4d1dec256v32_chain_decode.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, ctypes.c_uint32, c_vp, c_vp, c_vp]
         for name in ("tpf_p4dec256v32_batch", "tpf_p4d1dec256v32_batch", "tpf_p4enc256v32_batch",
                      "tpf_p4d1enc256v32_batch", "tpf_dec_batch", "tpf_enc_batch", "tpf_p4d1dec256v32_chained",
-                     "tpf_p4d1dec256v32_chain_sums", "tpf_p4d1dec256v32_chain_decode"):
+                     "tpf_p4d1dec256v32_chain_sums", "tpf_p4d1dec256v32_chain_decode", "tpf_probe256v32"):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -103,6 +104,15 @@ def dec256v32(packed, offsets, nblocks, out=None, starts=None, err=None):
         rc = L.tpf_p4d1dec256v32_batch(_ptr(packed), packed.numel(), _ptr(offsets), nblocks, _ptr(out),
                                        _ptr(starts), _ptr(err), _stream(torch))
     _check(rc)
+    return out
+
+
+def probe256v32(packed, offsets, nblocks, out):
+    """Measurement only: the decode kernel's loads and stores without the
+    decoding (data-movement ceiling of the hot path's access pattern)."""
+    import torch
+
+    _check(lib().tpf_probe256v32(_ptr(packed), packed.numel(), _ptr(offsets), nblocks, _ptr(out), _stream(torch)))
     return out
 
 
