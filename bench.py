@@ -359,12 +359,13 @@ def run_c3(args, world, rank, dev, T, chained):
             f"vbyte-mode blocks {vb_frac:.1%}")
     out = torch.empty((nb, 256), dtype=torch.int32, device=dev)
     if chained:
+        # phase A (block sums + scan), [all-gather of one u32 per rank], phase B
         chain = tpf.D1Chain(packed, offs, nb)
-        start0 = int(starts[0].item()) if rank == 0 else 0
+        start0 = int(starts[0].item()) & 0xFFFFFFFF
 
         def step():
             chain.sums()
-            base = tpf_shard.chained_base(chain.total, start0=0) if world > 1 else 0
+            base = tpf_shard.chained_base(chain.total, start0=start0) if world > 1 else start0
             chain.decode(base, out=out)
 
         fn = step
@@ -380,7 +381,8 @@ def run_c3(args, world, rank, dev, T, chained):
     roof = {"bound": "hbm", "achieved": round(alg / (avg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
             "kernel_ms_avg": round(avg_ms, 4),
-            "kernel": ("chain_sums + chain_decode" if chained else "tpf::dev::k_dec256v32w<StartMode::PerBlock>")}
+            "kernel": ("k_dec256v32w<SumOnly> + hipcub scan + k_dec256v32w<Prefix>" if chained
+                       else "tpf::dev::k_dec256v32w<StartMode::PerBlock>")}
     cfg = {"workload": "C3: p4D1Dec256v32 " + ("chained list (start0 only)" if chained else "per-block starts")
                        + ", Zipf(1.1) gaps on [1,64] + 5% 64+U[0,2^16)",
            "nblocks_per_gpu": nb, "bytes_per_int": round(pbytes / nb / 256, 4), "vbyte_block_frac": round(vb_frac, 4),

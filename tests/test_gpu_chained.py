@@ -20,9 +20,10 @@ def _list(nb, start0, seed):
     return vals, starts
 
 
-@pytest.mark.parametrize("start0", [0, 7, 0xFFFFFF00])
-def test_chained_single(start0):
-    vals, starts = _list(5000, start0, seed=3)
+@pytest.mark.parametrize("start0,nb", [(0, 5000), (7, 5000), (0xFFFFFF00, 5000), (5, 1), (5, 3), (5, 4), (5, 5),
+                                       (5, 257), (11, 200003)])
+def test_chained_single(start0, nb):
+    vals, starts = _list(nb, start0, seed=3)
     packed_np, off_np = oracle_lib.enc256v32_batch(vals, starts=starts)
     packed = torch.from_numpy(packed_np).to(DEV)
     offs = torch.from_numpy(off_np.astype(np.int64)).to(DEV)
@@ -31,6 +32,18 @@ def test_chained_single(start0):
     torch.cuda.synchronize()
     assert int(err.item()) == -1
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), vals)
+
+
+def test_chained_corrupt_offsets():
+    vals, starts = _list(3000, 1, seed=5)
+    packed_np, off_np = oracle_lib.enc256v32_batch(vals, starts=starts)
+    off_bad = off_np.astype(np.int64).copy()
+    off_bad[1234] += 1  # blocks 1233 and 1234 disagree with their headers
+    packed = torch.from_numpy(packed_np).to(DEV)
+    err = torch.zeros(1, dtype=torch.int64, device=DEV)
+    tpf.dec256v32_chained(packed, torch.from_numpy(off_bad).to(DEV), len(vals), start0=1, err=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 1233
 
 
 def test_chained_sharded_exchange():

@@ -7,7 +7,7 @@
 // __syncthreads; it was latency-bound (one tile in flight per workgroup,
 // 39% of HBM peak).  The kernel below runs every wave independently with a
 // software pipeline and no workgroup barrier.
-#include "p4_block32.h"
+#include "p4_dec_run.h"
 #include "tpf_kernels.h"
 
 #include <hipcub/hipcub.hpp>
@@ -46,56 +46,17 @@ struct DecArgs
 // 16-byte buffer loads per lane = up to 2 KB per block).  Three register
 // chunks rotate (loop unrolled by three) so no in-flight load result is ever
 // copied (a copy forces s_waitcnt vmcnt(0)).  No workgroup barriers at all.
-//
-// Control plane in vector lanes: the run's offsets arrive with one vector load
-// (lane j = block first+j) and every per-block quantity the loop needs (chunk
-// base, span, byte offset inside the chunk, expected length, start value) is
-// computed once per run in VALU and fetched per block with v_readlane.  The
-// scalar unit is shared by the CU's four SIMDs; per-block 64-bit address
-// arithmetic on it was the measured limiter.
-constexpr uint32_t kSlotBytes = 2304 + 64;
-constexpr uint32_t kRunDefault = 16; // blocks per wave (<= 62: lanes >= n hold "no block")
-
-// ctl word bits
-constexpr uint32_t kCtlSpan = 0xFFFu;    // bytes the fast path stages (0: none)
-constexpr uint32_t kCtlShift = 12;       // [12,16): block start inside its 16-aligned chunk
-constexpr uint32_t kCtlSlow = 1u << 16;  // > 2 KB or straddles the stream end: guarded loads
-constexpr uint32_t kCtlTwo = 1u << 17;   // second 1 KB half present
-
-struct Chunk
-{
-    u32x4 a, b; // bytes [0,1024) and [1024,2048) of the 16-aligned block image
-};
-
-__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane)
-{
-    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(lane)));
-}
-
-// POL (A/B knob): bit 0 = non-temporal loads (measured -4%), bit 1 =
-// non-temporal stores (measured +2.5%, default), bit 2 = block order.
-template <uint32_t POL>
-__device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t off)
-{
-    return __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), 0, (POL & 1u) ? 2 : 0);
-}
-
-template <uint32_t POL>
-__device__ __forceinline__ void st16(u32x4 * p, const u32x4 & v)
-{
-    if constexpr ((POL & 2u) != 0u)
-        __builtin_nontemporal_store(v, p);
-    else
-        *p = v;
-}
-
-template <StartMode SM, uint32_t kRun, uint32_t POL = 0>
-__global__ __launch_bounds__(256, 7) void k_dec256v32w(const DecArgs A)
+// The run's control plane lives in vector lanes (RunPlane, p4_dec_run.h).
+// Measured and kept: runs of 16 (8: same, 32..62: -2..-5%),
+// three chunks at 7 waves/SIMD (four at 6: same).
+template <StartMode SM, uint32_t kRun, uint32_t POL = 2, uint32_t NC = 3, int MINW = 7>
+__global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
 {
     __shared__ uint32_t slots[4][kSlotBytes / 4];
     __shared__ uint32_t scratch[4][kWaveScratchU32];
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
+    const uint64_t wg = blockIdx.x;
     uint32_t * slot = slots[wv];
     uint32_t * scr = scratch[wv];
     const uint64_t in_base = reinterpret_cast<uint64_t>(A.in);
@@ -104,8 +65,7 @@ __global__ __launch_bounds__(256, 7) void k_dec256v32w(const DecArgs A)
     // POL bit 2: the workgroup's 4*kRun blocks are dealt to its waves
     // round-robin (block first + stride*j) instead of in contiguous runs.
     constexpr uint32_t stride = (POL & 4u) ? 4u : 1u;
-    const uint64_t first = (POL & 4u) ? static_cast<uint64_t>(blockIdx.x) * 4u * kRun + wv
-                                      : (static_cast<uint64_t>(blockIdx.x) * 4u + wv) * kRun;
+    const uint64_t first = (POL & 4u) ? wg * 4u * kRun + wv : (wg * 4u + wv) * kRun;
     if (first >= A.nblocks)
         return;
     const uint32_t n = static_cast<uint32_t>(min_u64(kRun, (A.nblocks - first + stride - 1u) / stride));
@@ -115,15 +75,8 @@ __global__ __launch_bounds__(256, 7) void k_dec256v32w(const DecArgs A)
     const uint64_t blk = first + stride * t;
     const uint64_t o = valid ? A.off[blk] : 0ull;
     const uint64_t e = valid ? A.off[blk + 1u] : 0ull;
-    const uint64_t ab = in_base + o;
-    const uint64_t cb = ab & ~15ull;
-    const uint32_t span = valid ? static_cast<uint32_t>(min_u64(sub_sat(in_base + e, cb), kSlotBytes - 64)) : 0u;
-    const uint32_t avail = valid ? static_cast<uint32_t>(min_u64(sub_sat(in_end, cb), kSlotBytes)) : 0u;
-    const bool slow = valid && (span > 2048u || span + 16u > avail);
-    const uint32_t ctlv = (slow ? 0u : span) | ((static_cast<uint32_t>(ab) & 15u) << kCtlShift) | (slow ? kCtlSlow : 0u)
-        | (!slow && span > 1024u ? kCtlTwo : 0u);
-    const uint32_t lenv = (e >= o && e - o < 0x10000ull) ? static_cast<uint32_t>(e - o) : 0xFFFFFFFFu;
-    const uint32_t cblo = static_cast<uint32_t>(cb), cbhi = static_cast<uint32_t>(cb >> 32);
+    RunPlane P;
+    P.init(in_base, in_end, o, e, valid);
     uint32_t startv = 0u;
     if constexpr (SM == StartMode::PerBlock)
         startv = valid ? A.starts[blk] : 0u;
@@ -132,41 +85,19 @@ __global__ __launch_bounds__(256, 7) void k_dec256v32w(const DecArgs A)
     uint32_t sumv = 0u;
     uint32_t * const out_run = SM == StartMode::SumOnly ? nullptr : A.out + first * 256u;
     uint64_t badmask = 0u;
+    constexpr bool sum_pass = SM == StartMode::SumOnly;
 
-    auto issue = [&](Chunk & c, uint32_t jj) {
-        // jj <= n + 1 <= 63: lanes >= n have ctl 0 (no bytes, no traffic)
-        const uint32_t ctl = rl(ctlv, jj);
-        const uint64_t base = (static_cast<uint64_t>(rl(cbhi, jj)) << 32) | rl(cblo, jj);
-        const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(base), kSlotBytes);
-        const uint32_t fspan = ctl & kCtlSpan;
-        c.a = ld16<POL>(rs, 16u * t < fspan ? 16u * t : 0x80000000u);
-        c.b = ld16<POL>(rs, 1024u + 16u * t < fspan ? 1024u + 16u * t : 0x80000000u);
-    };
+    auto issue = [&](Chunk & c, uint32_t jj) { P.issue<POL>(c, jj, t); };
     auto consume = [&](const Chunk & c, uint32_t jj) {
-        const uint32_t ctl = rl(ctlv, jj);
         if constexpr (SM == StartMode::Probe)
         {
             st16<POL>(reinterpret_cast<u32x4 *>(out_run + jj * stride * 256u) + t, c.a | c.b);
             return;
         }
-        reinterpret_cast<u32x4 *>(slot)[t] = c.a;
-        if (ctl & kCtlTwo)
-            reinterpret_cast<u32x4 *>(slot)[64 + t] = c.b;
-        if (ctl & kCtlSlow)
-        {
-            // rare: > 2 KB blocks or the chunk straddling the end of the stream
-            // (a raw buffer load that crosses num_records returns 0)
-            const uint32_t sp = rl(span, jj), av = rl(avail, jj);
-            const uint64_t base = (static_cast<uint64_t>(rl(cbhi, jj)) << 32) | rl(cblo, jj);
-            const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(base), av);
-            const uint8_t * bp = reinterpret_cast<const uint8_t *>(base);
-            for (uint32_t x = 16u * t; x < sp; x += 1024u)
-                reinterpret_cast<u32x4 *>(slot)[x >> 4] = load16_guarded(bp, rs, x, av);
-        }
-        wave_lds_sync();
+        const uint32_t ctl = P.stage(c, jj, slot, t);
         u32x4 v;
         const uint32_t used = decode_block256v32(slot, (ctl >> kCtlShift) & 15u, scr, t, v);
-        if constexpr (SM == StartMode::SumOnly)
+        if constexpr (sum_pass)
         {
             const uint32_t s = wave_sum(v.x + v.y + v.z + v.w + 4u);
             sumv = t == jj ? s : sumv;
@@ -178,28 +109,33 @@ __global__ __launch_bounds__(256, 7) void k_dec256v32w(const DecArgs A)
             st16<POL>(reinterpret_cast<u32x4 *>(out_run + jj * stride * 256u) + t, v);
         }
         wave_lds_sync();
-        if (used != rl(lenv, jj))
+        if (used != rl(P.len, jj))
             badmask |= 1ull << jj;
     };
 
-    Chunk C0, C1, C2;
-    issue(C0, 0);
-    issue(C1, 1);
-    for (uint32_t j = 0;; j += 3)
-    {
-        issue(C2, j + 2);
-        consume(C0, j);
-        if (j + 1 >= n)
-            break;
-        issue(C0, j + 3);
-        consume(C1, j + 1);
-        if (j + 2 >= n)
-            break;
-        issue(C1, j + 4);
-        consume(C2, j + 2);
-        if (j + 3 >= n)
-            break;
-    }
+    // NC register chunks rotate (loop unrolled by NC, no copies): while block
+    // j is decoded, blocks j+1 .. j+NC-1 are in flight.
+    auto run_pass = [&]() {
+        Chunk C[NC];
+#pragma unroll
+        for (uint32_t u = 0; u + 1 < NC; ++u)
+            issue(C[u], u);
+        bool more = true;
+        for (uint32_t j = 0; more; j += NC)
+        {
+#pragma unroll
+            for (uint32_t u = 0; u < NC; ++u)
+            {
+                if (more)
+                {
+                    issue(C[(u + NC - 1) % NC], j + u + NC - 1);
+                    consume(C[u], j + u);
+                    more = j + u + 1 < n;
+                }
+            }
+        }
+    };
+    run_pass();
     if constexpr (SM == StartMode::SumOnly)
     {
         if (valid)
@@ -216,18 +152,12 @@ namespace tpf
 
 namespace
 {
-// A/B knobs (defaults = measured best): TPF_DEC_RUN blocks per wave run,
-// TPF_DEC_POL cache policy bits (see ld16/st16).
+// A/B knob (default = measured best): TPF_DEC_POL cache policy / block order
+// bits (see ld16/st16 in p4_dec_run.h).
 uint32_t env_knob(const char * name, uint32_t dflt)
 {
     const char * e = std::getenv(name);
     return e ? static_cast<uint32_t>(std::atoi(e)) : dflt;
-}
-
-uint32_t dec_run()
-{
-    static const uint32_t v = env_knob("TPF_DEC_RUN", dev::kRunDefault) == 8 ? 8u : 16u;
-    return v;
 }
 
 uint32_t dec_pol()
@@ -236,19 +166,13 @@ uint32_t dec_pol()
     return v;
 }
 
-template <dev::StartMode SM, uint32_t RUN, uint32_t POL>
-hipError_t launch_run(const dev::DecArgs & A, hipStream_t stream)
-{
-    const uint64_t per_wg = 4ull * RUN;  // both block orders cover 4*RUN blocks per workgroup
-    const uint32_t grid = static_cast<uint32_t>((A.nblocks + per_wg - 1) / per_wg);
-    hipLaunchKernelGGL((dev::k_dec256v32w<SM, RUN, POL>), dim3(grid), dim3(256), 0, stream, A);
-    return hipGetLastError();
-}
-
 template <dev::StartMode SM, uint32_t POL>
 hipError_t launch_pol(const dev::DecArgs & A, hipStream_t stream)
 {
-    return dec_run() == 8 ? launch_run<SM, 8, POL>(A, stream) : launch_run<SM, 16, POL>(A, stream);
+    constexpr uint64_t per_wg = 4ull * dev::kRunDefault;
+    const uint32_t grid = static_cast<uint32_t>((A.nblocks + per_wg - 1) / per_wg);
+    hipLaunchKernelGGL((dev::k_dec256v32w<SM, dev::kRunDefault, POL>), dim3(grid), dim3(256), 0, stream, A);
+    return hipGetLastError();
 }
 
 template <dev::StartMode SM>

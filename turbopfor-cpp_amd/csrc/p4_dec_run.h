@@ -1,0 +1,112 @@
+// p4_dec_run.h -- per-wave run machinery shared by the 256v32 decode kernels
+// (p4_dec256v32.hip, p4_d1chain.hip): the run's control plane held in vector
+// lanes, the register-chunk loads and the LDS staging of one block.
+#pragma once
+
+#include "p4_block32.h"
+
+namespace tpf::dev
+{
+
+constexpr uint32_t kSlotBytes = 2304 + 64;
+constexpr uint32_t kRunDefault = 16; // blocks per wave (<= 62: lanes >= n hold "no block")
+
+// ctl word bits
+constexpr uint32_t kCtlSpan = 0xFFFu;    // bytes the fast path stages (0: none)
+constexpr uint32_t kCtlShift = 12;       // [12,16): block start inside its 16-aligned chunk
+constexpr uint32_t kCtlSlow = 1u << 16;  // > 2 KB or straddles the stream end: guarded loads
+constexpr uint32_t kCtlTwo = 1u << 17;   // second 1 KB half present
+
+struct Chunk
+{
+    u32x4 a, b; // bytes [0,1024) and [1024,2048) of the 16-aligned block image
+};
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane)
+{
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(lane)));
+}
+
+// POL (A/B knob): bit 0 = non-temporal loads (measured -4%), bit 1 =
+// non-temporal stores (measured +2.5%, default), bit 2 = block order.
+template <uint32_t POL>
+__device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    return __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), 0, (POL & 1u) ? 2 : 0);
+}
+
+template <uint32_t POL>
+__device__ __forceinline__ void st16(u32x4 * p, const u32x4 & v)
+{
+    if constexpr ((POL & 2u) != 0u)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+// Control plane of a run of up to 62 blocks, lane j = the run's j-th block:
+// the run's offsets arrive with one vector load and every per-block quantity
+// (chunk base, span, byte offset inside the chunk, expected length) is
+// computed once in VALU and fetched per block with v_readlane.  The scalar
+// unit is shared by the CU's four SIMDs; per-block 64-bit address arithmetic
+// on it was the measured limiter before this layout.
+struct RunPlane
+{
+    uint32_t ctl;        // kCtl* bits
+    uint32_t len;        // expected byte length (0xFFFFFFFF: implausible offsets)
+    uint32_t cblo, cbhi; // 16-aligned chunk base address
+    uint32_t span;       // bytes to stage
+    uint32_t avail;      // readable bytes from the chunk base (stream end)
+
+    __device__ __forceinline__ void init(uint64_t in_base, uint64_t in_end, uint64_t o, uint64_t e, bool valid)
+    {
+        const uint64_t ab = in_base + o;
+        const uint64_t cb = ab & ~15ull;
+        span = valid ? static_cast<uint32_t>(min_u64(sub_sat(in_base + e, cb), kSlotBytes - 64)) : 0u;
+        avail = valid ? static_cast<uint32_t>(min_u64(sub_sat(in_end, cb), kSlotBytes)) : 0u;
+        const bool slow = valid && (span > 2048u || span + 16u > avail);
+        ctl = (slow ? 0u : span) | ((static_cast<uint32_t>(ab) & 15u) << kCtlShift) | (slow ? kCtlSlow : 0u)
+            | (!slow && span > 1024u ? kCtlTwo : 0u);
+        len = (e >= o && e - o < 0x10000ull) ? static_cast<uint32_t>(e - o) : 0xFFFFFFFFu;
+        cblo = static_cast<uint32_t>(cb);
+        cbhi = static_cast<uint32_t>(cb >> 32);
+    }
+
+    // Two unconditional 16-byte loads per lane (block jj's bytes [0,2048));
+    // lanes past the block, and blocks jj >= n (ctl 0), get an out-of-range
+    // offset: zeros, no memory traffic, and the same vmcnt pattern on every path.
+    template <uint32_t POL>
+    __device__ __forceinline__ void issue(Chunk & c, uint32_t jj, uint32_t t) const
+    {
+        const uint32_t cw = rl(ctl, jj);
+        const uint64_t base = (static_cast<uint64_t>(rl(cbhi, jj)) << 32) | rl(cblo, jj);
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(base), kSlotBytes);
+        const uint32_t fspan = cw & kCtlSpan;
+        c.a = ld16<POL>(rs, 16u * t < fspan ? 16u * t : 0x80000000u);
+        c.b = ld16<POL>(rs, 1024u + 16u * t < fspan ? 1024u + 16u * t : 0x80000000u);
+    }
+
+    // Write block jj's chunk into the wave's LDS slot; returns its ctl word.
+    __device__ __forceinline__ uint32_t stage(const Chunk & c, uint32_t jj, uint32_t * slot, uint32_t t) const
+    {
+        const uint32_t cw = rl(ctl, jj);
+        reinterpret_cast<u32x4 *>(slot)[t] = c.a;
+        if (cw & kCtlTwo)
+            reinterpret_cast<u32x4 *>(slot)[64 + t] = c.b;
+        if (cw & kCtlSlow)
+        {
+            // rare: > 2 KB blocks or the chunk straddling the end of the stream
+            // (a raw buffer load that crosses num_records returns 0)
+            const uint32_t sp = rl(span, jj), av = rl(avail, jj);
+            const uint64_t base = (static_cast<uint64_t>(rl(cbhi, jj)) << 32) | rl(cblo, jj);
+            const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(base), av);
+            const uint8_t * bp = reinterpret_cast<const uint8_t *>(base);
+            for (uint32_t x = 16u * t; x < sp; x += 1024u)
+                reinterpret_cast<u32x4 *>(slot)[x >> 4] = load16_guarded(bp, rs, x, av);
+        }
+        wave_lds_sync();
+        return cw;
+    }
+};
+
+} // namespace tpf::dev

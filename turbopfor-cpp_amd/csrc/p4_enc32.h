@@ -39,13 +39,6 @@ __device__ __forceinline__ uint32_t vblen32(uint32_t x)
     return x < 156u ? 1u : x < 16540u ? 2u : x < 2113692u ? 3u : x <= 0xFFFFFFu ? 4u : 5u;
 }
 
-__device__ __forceinline__ uint32_t wave_min(uint32_t x)
-{
-    for (uint32_t d = 1; d < 64; d <<= 1)
-        x = min(x, static_cast<uint32_t>(__shfl_xor(static_cast<int>(x), d, 64)));
-    return x;
-}
-
 // hist: per-wave LDS scratch of >= 64 u32.
 __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist, uint32_t t)
 {

@@ -141,7 +141,7 @@ __device__ __forceinline__ uint32_t vbyte_len(uint32_t m)
 }
 
 // vbyte exceptions into scr[pos] (T per position, zeroed here).  Same
-// window/ballot parse as vbyte_exceptions in p4_block32.h, generic width.
+// 64-byte window parse as vbyte_exceptions in p4_block32.h, generic width.
 template <bool Wide>
 __device__ __forceinline__ uint32_t vbyte_exceptions_g(const uint32_t * lds, uint32_t v0, uint32_t xn,
                                                        typename std::conditional<Wide, uint64_t, uint32_t>::type * scr,
@@ -167,41 +167,24 @@ __device__ __forceinline__ uint32_t vbyte_exceptions_g(const uint32_t * lds, uin
     }
     else
     {
+        // value starts by binary lifting (window_starts, p4_block32.h)
         uint32_t c = v0, sp = 0, found = 0;
         vend = v0;
         while (found < xn)
         {
-            const uint32_t by = lds_byte(lds, c + t);
-            const uint32_t len = vbyte_len<Wide>(by);
-            uint64_t Lk[8];
-#pragma unroll
-            for (uint32_t q = 0; q < 8; ++q)
-                Lk[q] = __ballot(len >= q + 2u);
-            const uint32_t need = xn - found;
-            uint64_t M = 0;
-            uint32_t cnt = 0;
-            while (sp < 64u && cnt < need)
-            {
-                M |= 1ull << sp;
-                ++cnt;
-                uint32_t l = 1u;
-#pragma unroll
-                for (uint32_t q = 0; q < 8; ++q)
-                    l += static_cast<uint32_t>((Lk[q] >> sp) & 1ull);
-                sp += l;
-            }
-            if ((M >> t) & 1ull)
-            {
-                const uint32_t k = found + __builtin_popcountll(M & lanemask_lt());
-                tmp[k & 255u] = static_cast<T>(vbyte_value<Wide>(lds, c + t, by));
-            }
+            const uint32_t nxt = t + vbyte_len<Wide>(lds_byte(lds, c + t));
+            const uint32_t p = window_starts(nxt, sp, t);
+            const uint32_t m = static_cast<uint32_t>(__builtin_popcountll(__ballot(p < 64u)));
+            const uint32_t cnt = min(m, xn - found);
+            const uint32_t pn = bperm(nxt, p); // every lane: bpermute reads 0 from inactive lanes
+            const uint32_t pe = p < 64u ? pn : p;
+            if (t < cnt)
+                tmp[(found + t) & 255u] = static_cast<T>(vbyte_value<Wide>(lds, c + p, lds_byte(lds, c + p)));
+            const uint32_t e_last = uni(__builtin_amdgcn_readlane(pe, cnt - 1u));
             found += cnt;
-            vend = c + sp;
-            if (sp >= 64u)
-            {
-                sp -= 64u;
-                c += 64u;
-            }
+            vend = c + e_last;
+            sp = e_last >= 64u ? e_last - 64u : e_last;
+            c += e_last >= 64u ? 64u : 0u;
         }
         wave_lds_sync();
         for (uint32_t k = t; k < xn; k += 64u)

@@ -108,11 +108,32 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x)
     return __builtin_amdgcn_readlane(s, 63);
 }
 
+// Wave-wide OR / unsigned min, result in every lane: DPP inclusive scan
+// (VALU, a few cycles per step) then a broadcast of lane 63 -- the
+// __shfl_xor butterfly would be six ds_bpermute round trips through LDS.
 __device__ __forceinline__ uint32_t wave_or(uint32_t x)
 {
-    for (uint32_t d = 1; d < 64; d <<= 1)
-        x |= __shfl_xor(x, d, 64);
-    return x;
+    x |= __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false); // row_shr:1
+    x |= __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false); // row_shr:2
+    x |= __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false); // row_shr:4
+    x |= __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false); // row_shr:8
+    x |= __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false); // row_bcast:15
+    x |= __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false); // row_bcast:31
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), 63));
+}
+
+__device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
+
+__device__ __forceinline__ uint32_t wave_min(uint32_t x)
+{
+    constexpr uint32_t I = 0xFFFFFFFFu; // identity for lanes without a source
+    x = umin32(x, __builtin_amdgcn_update_dpp(I, x, 0x111, 0xf, 0xf, false));
+    x = umin32(x, __builtin_amdgcn_update_dpp(I, x, 0x112, 0xf, 0xf, false));
+    x = umin32(x, __builtin_amdgcn_update_dpp(I, x, 0x114, 0xf, 0xf, false));
+    x = umin32(x, __builtin_amdgcn_update_dpp(I, x, 0x118, 0xf, 0xf, false));
+    x = umin32(x, __builtin_amdgcn_update_dpp(I, x, 0x142, 0xa, 0xf, false));
+    x = umin32(x, __builtin_amdgcn_update_dpp(I, x, 0x143, 0xc, 0xf, false));
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), 63));
 }
 
 __device__ __forceinline__ uint64_t lanemask_lt()

@@ -227,7 +227,20 @@ class D1Chain:
         return out
 
 
-def dec256v32_chained(packed, offsets, nblocks, start0=0, out=None, err=None):
-    c = D1Chain(packed, offsets, nblocks)
-    c.sums(err=err)
-    return c.decode(start0, out=out)
+def dec256v32_chained(packed, offsets, nblocks, start0=0, out=None, err=None, ws=None):
+    """One chained list (block i starts from block i-1's last value, block 0
+    from start0): tpf_p4d1dec256v32_chained (block sums + scan, then decode).
+    ws: optional reusable uint8 workspace tensor."""
+    import torch
+
+    if out is None:
+        out = torch.empty((nblocks, 256), dtype=torch.int32, device=packed.device)
+    L = lib()
+    ws_bytes = int(L.tpf_p4d1dec256v32_chain_workspace_size(nblocks))
+    if ws is None or ws.numel() < ws_bytes:
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=packed.device)
+    rc = L.tpf_p4d1dec256v32_chained(_ptr(packed), packed.numel(), _ptr(offsets), nblocks, _ptr(out),
+                                     ctypes.c_uint32(start0 & 0xFFFFFFFF), _ptr(ws), ws.numel(), _ptr(err),
+                                     _stream(torch))
+    _check(rc)
+    return out
