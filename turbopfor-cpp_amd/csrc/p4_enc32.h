@@ -39,7 +39,9 @@ __device__ __forceinline__ uint32_t vblen32(uint32_t x)
     return x < 156u ? 1u : x < 16540u ? 2u : x < 2113692u ? 3u : x <= 0xFFFFFFu ? 4u : 5u;
 }
 
-// hist: per-wave LDS scratch of >= 64 u32.
+// hist: per-wave LDS scratch of kPlanHistU32 u32 (16-byte aligned).
+using PlanHist = WaveHist<16, 36>; // bit widths 0..32
+constexpr uint32_t kPlanHistU32 = PlanHist::kU32;
 __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist, uint32_t t)
 {
     Plan32 P;
@@ -65,14 +67,15 @@ __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist
         P.raw = 0;
         return P;
     }
-    hist[t] = 0u;
+    PlanHist::zero(hist, t);
     wave_lds_sync();
-    atomicAdd(&hist[bw32(v.x)], 1u);
-    atomicAdd(&hist[bw32(v.y)], 1u);
-    atomicAdd(&hist[bw32(v.z)], 1u);
-    atomicAdd(&hist[bw32(v.w)], 1u);
+    PlanHist::add(hist, bw32(v.x), t);
+    PlanHist::add(hist, bw32(v.y), t);
+    PlanHist::add(hist, bw32(v.z), t);
+    PlanHist::add(hist, bw32(v.w), t);
     wave_lds_sync();
-    const uint32_t cnt = hist[t]; // lane c holds cnt[c] (0 for c > 32)
+    const uint32_t cnt = PlanHist::get(hist, t); // lane c holds cnt[c] (0 for c > 32)
+    wave_lds_sync();
     auto at = [&](uint32_t c) -> uint32_t {
         uint32_t x = static_cast<uint32_t>(__shfl(static_cast<int>(cnt), static_cast<int>(c & 63u), 64));
         return c < 64u ? x : 0u;
@@ -142,90 +145,152 @@ __device__ __forceinline__ void or_bits(uint32_t * img, uint32_t bp, uint32_t va
         atomicOr(&img[q + 1], val >> (32u - sh));
 }
 
-// Scatter the 4 values of lane t into the 256v32 base layout at byte p.
-__device__ __forceinline__ void pack256v32_lane(uint32_t * img, uint32_t p, uint32_t b, uint32_t t, const u32x4 & v)
+// ---- block image construction (write pass) --------------------------------
+// The image of one block is built in LDS so that its base payload starts on
+// a dword: the block starts at image byte sb = 4 + s0, s0 in [0,3] chosen
+// from the payload offset, and the copy-out shifts by bytes (v_alignbyte).
+// Each lane ORs RUNS of up to four consecutive values of one bit stream
+// (concatenated in registers first) into the image, so a dword receives few
+// atomic ORs: for the base payload lane t = 8l + r takes column l's groups
+// 4r..4r+3 (read back transposed from the staged values), for the bitmap
+// exceptions its own exceptions, which are consecutive ranks.  The first
+// version OR-ed every value separately (32 lanes into one dword at b = 1:
+// 162 SALU + 51 LDS-conflict cycles per block); a per-dword gather variant
+// was slower still (dependent LDS reads, 7.4 ms per 10M blocks).
+
+constexpr uint32_t kEncValU32 = 256; // staged masked base values, element order
+
+// OR cnt (<= 4) consecutive nb-bit values x[] (each < 2^nb) into a bit stream
+// at stream bit `bit`; stream dword i lives at img[dw0 + stride * i].  maxw:
+// a wave-uniform bound on the dwords a run touches (extra dwords get OR 0),
+// so the stores are not under divergent branches.
+__device__ __forceinline__ void or_run(uint32_t * img, uint32_t dw0, uint32_t stride, uint32_t bit, const uint32_t x[4],
+                                       uint32_t cnt, uint32_t nb, uint32_t maxw)
 {
-    if (b == 0u)
-        return;
-    const uint32_t m = mask32(b);
-    const uint32_t g = t >> 1;
-    const uint32_t o = g * b;
-    const uint32_t k = o >> 5, sh = o & 31u;
-    const uint32_t lane0 = 4u * (t & 1u);
-    const uint32_t vals[4] = {v.x & m, v.y & m, v.z & m, v.w & m};
+    // 128-bit concatenation (lo, hi) of the run
+    uint64_t lo = 0, hi = 0;
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j)
     {
-        const uint32_t l = lane0 + j;
-        const uint32_t lo_byte = p + 32u * k + 4u * l;
-        const uint32_t x = vals[j];
-        const uint32_t lo_bits = min(b, 32u - sh);
-        or_bits(img, lo_byte * 8u + sh, x & mask32(lo_bits), lo_bits);
-        if (b > lo_bits)
-            or_bits(img, (lo_byte + 32u) * 8u, x >> lo_bits, b - lo_bits);
+        const uint64_t xj = j < cnt ? x[j] : 0u;
+        const uint32_t pos = j * nb;
+        if (pos < 64u)
+        {
+            lo |= xj << pos;
+            if (pos + nb > 64u && pos > 0u)
+                hi |= xj >> (64u - pos);
+        }
+        else
+            hi |= xj << (pos - 64u);
     }
+    const uint32_t sh = bit & 31u, q = bit >> 5;
+    // shift the 128-bit run left by sh into five dwords
+    const uint32_t d0 = static_cast<uint32_t>(lo), d1 = static_cast<uint32_t>(lo >> 32);
+    const uint32_t d2 = static_cast<uint32_t>(hi), d3 = static_cast<uint32_t>(hi >> 32);
+    uint32_t w[5];
+    w[0] = d0 << sh;
+    w[1] = sh ? __builtin_amdgcn_alignbit(d1, d0, 32u - sh) : d1;
+    w[2] = sh ? __builtin_amdgcn_alignbit(d2, d1, 32u - sh) : d2;
+    w[3] = sh ? __builtin_amdgcn_alignbit(d3, d2, 32u - sh) : d3;
+    w[4] = sh ? (d3 >> (32u - sh)) : 0u;
+#pragma unroll
+    for (uint32_t i = 0; i < 5; ++i)
+        if (i < maxw)
+            atomicOr(&img[dw0 + stride * (q + i)], w[i]);
 }
 
-// Build the encoded block in the LDS image (zeroed, image byte 0 == block
-// byte 0 shifted by `phase` bytes).  Returns nothing; size is P.size.
-__device__ __forceinline__ void emit_block256(uint32_t * img, uint32_t phase, const Plan32 & P, const u32x4 & v, uint32_t t)
+// dwords a run of cnt <= 4 nb-bit values can touch at any bit alignment
+__device__ __forceinline__ uint32_t run_maxw(uint32_t cnt, uint32_t nb) { return (31u + cnt * nb + 31u) >> 5; }
+
+// Base payload (256v32 layout) at image dword pw from the staged values:
+// word (k, l) at img[pw + 8k + l] holds bits [32k, 32k+32) of column l,
+// whose g-th value is element 8g + l.
+__device__ __forceinline__ void pack_base_runs(uint32_t * img, uint32_t pw, const uint32_t * val, uint32_t b, uint32_t t)
 {
-    const uint32_t b = P.b;
-    const uint32_t s = phase; // byte position of the header in the image
-    if (P.bx == 0u)
-    {
-        if (t == 0)
-            or_bits(img, s * 8u, b, 8);
-        pack256v32_lane(img, s + 1u, b, t, v);
+    if (b == 0u)
         return;
-    }
+    const uint32_t l = t >> 3, r = t & 7u;
+    const uint32_t e = 32u * r + l; // element of group 4r in column l
+    const uint32_t x[4] = {val[e], val[e + 8u], val[e + 16u], val[e + 24u]};
+    or_run(img, pw + l, 8u, 4u * r * b, x, 4u, b, run_maxw(4u, b));
+}
+
+// Build block image; returns sb (image byte of the block's first byte).
+// v: lane t's values 4t..4t+3 (after delta coding), P: plan, val: scratch.
+__device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val, const Plan32 & P, const u32x4 & v,
+                                                  uint32_t t)
+{
+    uint8_t * const ib = reinterpret_cast<uint8_t *>(img);
+    const uint32_t b = P.b;
     if (P.bx == 34u)
     {
         // constant block (p4enc256v32_scalar.cpp:183-190): ceil(b/8) value bytes
+        const uint32_t x = v.x & mask32(b);
         if (t == 0)
-        {
-            or_bits(img, s * 8u, 0xC0u | b, 8);
-            or_bits(img, (s + 1u) * 8u, v.x & mask32(b), b);
-        }
-        return;
+            ib[4] = static_cast<uint8_t>(0xC0u | b);
+        if (t < ((b + 7u) >> 3))
+            ib[5 + t] = static_cast<uint8_t>(x >> (8u * t));
+        return 4u;
     }
     const uint32_t m = mask32(b);
+    const uint32_t xbytes = P.bx <= 32u ? ((P.xn * P.bx + 7u) >> 3) : 0u;
+    const uint32_t po = P.bx == 0u ? 1u : (P.bx <= 32u ? 34u + xbytes : 2u); // payload offset in the block
+    const uint32_t sb = 4u + ((4u - (po & 3u)) & 3u);
+    const uint32_t pw = (sb + po) >> 2;
+    reinterpret_cast<u32x4 *>(val)[t] = u32x4{v.x & m, v.y & m, v.z & m, v.w & m};
+    if (P.bx == 0u)
+    {
+        if (t == 0)
+            ib[sb] = static_cast<uint8_t>(b);
+        wave_lds_sync();
+        pack_base_runs(img, pw, val, b, t);
+        return sb;
+    }
     const uint32_t f0 = v.x > m, f1 = v.y > m, f2 = v.z > m, f3 = v.w > m;
     const uint32_t my = f0 | (f1 << 1) | (f2 << 2) | (f3 << 3);
     const uint32_t cnt = f0 + f1 + f2 + f3;
     const uint32_t incl = wave_incl_scan(cnt);
     const uint32_t before = incl - cnt; // exceptions in elements < 4t
-    const u32x4 base = u32x4{v.x & m, v.y & m, v.z & m, v.w & m};
-    const uint32_t ex[4] = {v.x >> (b & 31u), v.y >> (b & 31u), v.z >> (b & 31u), v.w >> (b & 31u)};
+    const uint32_t sh = b & 31u;
+    const uint32_t ex[4] = {v.x >> sh, v.y >> sh, v.z >> sh, v.w >> sh};
     if (P.bx <= 32u)
     {
         // [0x80|b][bx][bitmap 32B][xn*bx bits horizontal][256v32 base]
+        const uint32_t mynext = static_cast<uint32_t>(__shfl_down(static_cast<int>(my), 1, 64));
         if (t == 0)
         {
-            or_bits(img, s * 8u, 0x80u | b, 8);
-            or_bits(img, (s + 1u) * 8u, P.bx, 8);
+            ib[sb] = static_cast<uint8_t>(0x80u | b);
+            ib[sb + 1u] = static_cast<uint8_t>(P.bx);
         }
-        or_bits(img, (s + 2u) * 8u + 4u * t, my, 4);
-        const uint32_t xs = (s + 34u) * 8u;
-        uint32_t k = before;
+        if ((t & 1u) == 0u)
+            ib[sb + 2u + (t >> 1)] = static_cast<uint8_t>(my | (mynext << 4));
+        wave_lds_sync();
+        pack_base_runs(img, pw, val, b, t);
+        // this lane's exceptions are the consecutive ranks before..before+cnt-1
+        // compact the flagged values to the front, in order (selects only)
+        uint32_t xr[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (uint32_t j = 0; j < 4; ++j)
-            if ((my >> j) & 1u)
-            {
-                or_bits(img, xs + k * P.bx, ex[j], P.bx);
-                ++k;
-            }
-        pack256v32_lane(img, s + 34u + ((P.xn * P.bx + 7u) >> 3), b, t, base);
-        return;
+        for (int j = 3; j >= 0; --j)
+        {
+            const bool fj = (my >> j) & 1u;
+            xr[3] = fj ? xr[2] : xr[3];
+            xr[2] = fj ? xr[1] : xr[2];
+            xr[1] = fj ? xr[0] : xr[1];
+            xr[0] = fj ? ex[j] : xr[0];
+        }
+        if (cnt != 0u) // lanes without exceptions share `before` with a neighbour: no zero ORs
+            or_run(img, 0u, 1u, (sb + 34u) * 8u + before * P.bx, xr, cnt, P.bx, run_maxw(4u, P.bx));
+        return sb;
     }
     // vbyte: [0x40|b][xn][256v32 base][V][positions]
     if (t == 0)
     {
-        or_bits(img, s * 8u, 0x40u | b, 8);
-        or_bits(img, (s + 1u) * 8u, P.xn, 8);
+        ib[sb] = static_cast<uint8_t>(0x40u | b);
+        ib[sb + 1u] = static_cast<uint8_t>(P.xn);
     }
-    pack256v32_lane(img, s + 2u, b, t, base);
-    const uint32_t v0 = s + 2u + 32u * b;
+    wave_lds_sync();
+    pack_base_runs(img, pw, val, b, t);
+    const uint32_t v0 = sb + 2u + 32u * b;
     if (P.raw)
     {
         if (t == 0)
@@ -239,7 +304,7 @@ __device__ __forceinline__ void emit_block256(uint32_t * img, uint32_t phase, co
                 or_bits(img, (v0 + 1u + 4u * P.xn + k) * 8u, 4u * t + j, 8);
                 ++k;
             }
-        return;
+        return sb;
     }
     uint32_t len[4];
     uint32_t mylen = 0;
@@ -283,6 +348,7 @@ __device__ __forceinline__ void emit_block256(uint32_t * img, uint32_t phase, co
         pos += len[j];
         ++k;
     }
+    return sb;
 }
 
 } // namespace tpf::dev

@@ -370,7 +370,9 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t l)
 
 // p4Bits32 / p4Bits64 (p4_scalar_internal.cpp:270-387, :538-652) evaluated
 // across lanes (see p4_enc32.h for the closed forms), plus the exact size of
-// the chosen encoding.  hist: per-wave LDS scratch of >= 72 u32.
+// the chosen encoding.  hist: per-wave LDS scratch of kPlanGHistU32 u32.
+using PlanGHist = WaveHist<4, 68>; // bit widths 0..64 (lane t reads bin t < 64, plus bin 64)
+constexpr uint32_t kPlanGHistU32 = PlanGHist::kU32;
 template <Fmt F>
 __device__ __forceinline__ PlanG plan_block_g(const typename FmtTraits<F>::T v[4], uint32_t n, uint32_t * hist, uint32_t t)
 {
@@ -403,17 +405,16 @@ __device__ __forceinline__ PlanG plan_block_g(const typename FmtTraits<F>::T v[4
         P.size = 1u + ((maxb + 7u) >> 3);
         return P;
     }
-    hist[t] = 0u;
-    if (t < 8u)
-        hist[64u + t] = 0u;
+    PlanGHist::zero(hist, t);
     wave_lds_sync();
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j)
         if (t + 64u * j < n)
-            atomicAdd(&hist[bw64d(v[j])], 1u);
+            PlanGHist::add(hist, bw64d(v[j]), t);
     wave_lds_sync();
-    const uint32_t cnt = hist[t];
-    const uint32_t cnt64 = uni(hist[64]);
+    const uint32_t cnt = PlanGHist::get(hist, t);
+    const uint32_t cnt64 = uni(PlanGHist::get(hist, 64));
+    wave_lds_sync();
     auto at = [&](uint32_t c) -> uint32_t {
         const uint32_t x = static_cast<uint32_t>(__shfl(static_cast<int>(cnt), static_cast<int>(c & 63u), 64));
         return c < 64u ? x : (c == 64u ? cnt64 : 0u);

@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) void k_enc_g(const typename FmtTraits<F>::T * 
     using G = UnitGeom<F, PAIR>;
     using T = typename FmtTraits<F>::T;
     __shared__ uint32_t imgs[WRITE ? 4 : 1][WRITE ? (G::kSlot / 4 + 8) : 1];
-    __shared__ uint32_t hist[4][80];
+    __shared__ __attribute__((aligned(16))) uint32_t hist[4][kPlanGHistU32];
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
     const uint64_t W = static_cast<uint64_t>(gridDim.x) * 4u;

@@ -142,6 +142,41 @@ __device__ __forceinline__ uint64_t lanemask_lt()
     return t == 0 ? 0ull : (~0ull >> (64u - t));
 }
 
+// ---- wave histogram of small keys -----------------------------------------
+// C copies laid out [bin][C]; lane t adds into copy t % C, so lanes that share
+// a bin hit C different banks (64/C lanes per address at worst) instead of one
+// address 256 times: same-address LDS atomics serialise (measured 110 conflict
+// cycles per block with a single copy).  Scratch: NBINS*C u32, 16-B aligned.
+template <uint32_t C, uint32_t NBINS>
+struct WaveHist
+{
+    static constexpr uint32_t kU32 = NBINS * C;
+
+    __device__ __forceinline__ static void zero(uint32_t * h, uint32_t t)
+    {
+        for (uint32_t i = t; i < kU32 / 4u; i += 64u)
+            reinterpret_cast<u32x4 *>(h)[i] = u32x4{0u, 0u, 0u, 0u};
+    }
+
+    __device__ __forceinline__ static void add(uint32_t * h, uint32_t bin, uint32_t t)
+    {
+        atomicAdd(&h[bin * C + (t & (C - 1u))], 1u);
+    }
+
+    // count of `bin` (bins >= NBINS read as 0)
+    __device__ __forceinline__ static uint32_t get(const uint32_t * h, uint32_t bin)
+    {
+        if (bin >= NBINS)
+            return 0u;
+        const u32x4 * p = reinterpret_cast<const u32x4 *>(h + bin * C);
+        u32x4 s = p[0];
+#pragma unroll
+        for (uint32_t i = 1; i < C / 4u; ++i)
+            s += p[i];
+        return (s.x + s.y) + (s.z + s.w);
+    }
+};
+
 // ---- buffer loads: OOB lanes read zeros (no fault, no slack required) -----
 // Descriptor inputs are forced through readfirstlane so the compiler can
 // prove the SRD wave-uniform (otherwise every buffer op is wrapped in a
