@@ -64,3 +64,25 @@ def test_chained_sharded_exchange():
         base = (start0 + sum(totals[:r])) & 0xFFFFFFFF
         out = c.decode(base)
         np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), vals[lo:hi], err_msg=f"shard {r}")
+
+
+def test_chained_ws_reuse_and_modes():
+    """Same workspace across calls (status words re-zeroed per launch) and a
+    list mixing bitmap-, vbyte- and constant-mode blocks."""
+    rng = np.random.default_rng(12)
+    nb = 40000
+    gaps = rng.integers(0, 1 << rng.integers(0, 20, size=(nb, 1)), size=(nb, 256), dtype=np.uint64)
+    exc = rng.random((nb, 256)) < 0.1
+    gaps = np.where(exc, rng.integers(0, 1 << 31, size=(nb, 256), dtype=np.uint64), gaps)
+    gaps[::7] = 0  # constant blocks
+    flat = (np.cumsum(gaps.reshape(-1) + 1) + 3) & 0xFFFFFFFF
+    vals = flat.astype(np.uint32).reshape(nb, 256)
+    start0 = 3
+    starts = np.concatenate([[start0], vals[:-1, -1]]).astype(np.uint32)
+    packed_np, off_np = oracle_lib.enc256v32_batch(vals, starts=starts)
+    packed = torch.from_numpy(packed_np).to(DEV)
+    offs = torch.from_numpy(off_np.astype(np.int64)).to(DEV)
+    ws = torch.empty(int(tpf.lib().tpf_p4d1dec256v32_chain_workspace_size(nb)), dtype=torch.uint8, device=DEV)
+    for _ in range(3):
+        out = tpf.dec256v32_chained(packed, offs, nb, start0=start0, ws=ws)
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), vals)

@@ -96,14 +96,15 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
         }
         const uint32_t ctl = P.stage(c, jj, slot, t);
         u32x4 v;
-        const uint32_t used = decode_block256v32(slot, (ctl >> kCtlShift) & 15u, scr, t, v);
+        uint32_t used;
         if constexpr (sum_pass)
         {
-            const uint32_t s = wave_sum(v.x + v.y + v.z + v.w + 4u);
+            const uint32_t s = dsum_block256v32(slot, (ctl >> kCtlShift) & 15u, t, used);
             sumv = t == jj ? s : sumv;
         }
         else
         {
+            used = decode_block256v32(slot, (ctl >> kCtlShift) & 15u, scr, t, v);
             if constexpr (SM == StartMode::PerBlock || SM == StartMode::Prefix)
                 apply_delta1_256(v, rl(startv, jj));
             st16<POL>(reinterpret_cast<u32x4 *>(out_run + jj * stride * 256u) + t, v);
