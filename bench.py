@@ -415,20 +415,34 @@ def run_c4(args, world, rank, dev, T):
     raw = torch.randint(-(1 << 63), (1 << 63) - 1, (nb64, 256), device=dev, generator=g, dtype=torch.int64)
     mask = torch.where(bw >= 64, torch.full_like(bw, -1), (torch.ones_like(bw) << bw) - 1)
     v64 = torch.where(torch.rand((nb64, 256), device=dev, generator=g) < 0.1, raw, raw & mask).contiguous()
-    st64 = {}
+    st64 = {"out": torch.empty(nb64 * 256, dtype=torch.int64, device=dev)}
 
     def rt64():
         p, o = tpf.enc_batch("256v64", v64.view(-1), nb64, 256)
-        st64["out"] = tpf.dec_batch("256v64", p, o, nb64, 256)
+        st64["p"], st64["o"] = p, o
+        tpf.dec_batch("256v64", p, o, nb64, 256, out=st64["out"])
 
-    el64, _ = T.run(rt64, max(2, args.steps // 4), 1)
+    s64 = max(2, args.steps // 4)
+    el64, _ = T.run(rt64, s64, 1)
     ok64 = bool(torch.equal(st64["out"].view(nb64, 256), v64))
+    # the two halves separately (kernel time, HIP events on the launch stream)
+    _, enc_ms = T.run(lambda: tpf.enc256v32(vals, out=enc_out), args.steps, 1)
+    _, dec_ms = T.run(lambda: tpf.dec256v32(state["p"], state["o"], nb, out=dec_out), args.steps, 1)
+    out64 = st64["out"]
+    _, enc64_ms = T.run(lambda: tpf.enc_batch("256v64", v64.view(-1), nb64, 256), s64, 1)
+    _, dec64_ms = T.run(lambda: tpf.dec_batch("256v64", st64["p"], st64["o"], nb64, 256, out=out64), s64, 1)
     if rank != 0:
         return None
     value = nb * 256 * world / (elapsed / args.steps) / 1e9
+    g = lambda n, ms: round(n * 256 / (float(np.mean(ms)) * 1e-3) / 1e9, 2)
+    p64 = int(st64["p"].numel())
     cfg = {"workload": "C4: p4Enc256v32 + p4Dec256v32 round trip, bw 1..32 segments cycling 0/5/10/25% exceptions",
            "nblocks_per_gpu": nb, "verified": ok,
-           "roundtrip_256v64": {"nblocks": nb64, "G_int64_per_s": round(nb64 * 256 / (el64 / max(2, args.steps // 4)) / 1e9, 2),
+           "enc256v32_G_int32_per_s": g(nb, enc_ms), "dec256v32_G_int32_per_s": g(nb, dec_ms),
+           "roundtrip_256v64": {"nblocks": nb64, "G_int64_per_s": round(nb64 * 256 / (el64 / s64) / 1e9, 2),
+                                "enc_G_int64_per_s": g(nb64, enc64_ms), "dec_G_int64_per_s": g(nb64, dec64_ms),
+                                "packed_bytes_per_block": round(p64 / nb64, 1),
+                                "dec_alg_GBps": round((p64 + nb64 * (2048 + 8)) / (float(np.mean(dec64_ms)) * 1e-3) / 1e9, 1),
                                 "verified": ok64}}
     return line("G int32/s device-resident p4Enc256v32+p4Dec256v32 round trip", value, "G int32/s", world, args.steps,
                 args.warmup, elapsed, "u32", "synthetic (GPU-generated)", cfg), ok and ok64

@@ -1,0 +1,222 @@
+// p4_dec256v64.hip -- batch decode of 128v64 / 256v64 P4 blocks (p4Dec128v64,
+// p4Dec256v64 and their D1 variants, reference
+// src/scalar/p4d1dec128v64_scalar.cpp:157-375, p4d1dec256v64_scalar.cpp:15-49)
+// on gfx950, with the run pipeline of the 256v32 hot path (p4_dec_run.h).
+//
+// A unit is one reference call: one 128v64 block (NB = 1) or the pair of
+// 128v64 blocks of a 256v64 call (NB = 2); offsets are per unit, so the second
+// block starts where the first one's parse ends.  Lane t owns the two
+// consecutive values 2t, 2t+1 of each 128-value block and writes them with
+// one 16-byte store (1 KB per block per wave, fully coalesced).
+// Base payload (bitunpack128v64Scalar, bitpack128v64_scalar.cpp:78-104):
+//   b <= 32: the 128v32 layout (4 interleaved lanes) of the pair-swapped low
+//            halves, element e at 128v32 index e ^ 2.  Elements 2t and 2t+1
+//            land in columns (t&1 ? 0 : 2) and +1 of group t>>1: one bit
+//            offset, two adjacent dwords per 16-byte word group;
+//   b >  32: a horizontal LSB-first 64-bit stream.
+// Header b = 63 means 64 (p4_scalar_internal.cpp:645-649).
+#include "p4_dec_run.h"
+#include "p4_generic.h"
+#include "tpf_kernels.h"
+
+namespace tpf::dev
+{
+
+// Worst-case unit: two vbyte-mode blocks with raw escape (2 + 16*62 + 1 + 8*128
+// + 128 = 2147 B each), staged from a 16-aligned chunk base.
+constexpr uint32_t kSlot64 = 4352 + 64;
+
+// Values 2t, 2t+1 of the 128v64 base payload at LDS byte p, width b.
+__device__ __forceinline__ void unpack128v64_lane(const uint32_t * lds, uint32_t p, uint32_t b, uint32_t t, uint64_t & x0,
+                                                  uint64_t & x1)
+{
+    if (b <= 32u)
+    {
+        const uint32_t o = (t >> 1) * b;
+        const uint32_t pos = p + 16u * (o >> 5) + ((t & 1u) ? 0u : 8u);
+        const uint32_t sh = o & 31u, m = p & 3u, q = pos >> 2;
+        const uint32_t d0 = lds[q], d1 = lds[q + 1], d2 = lds[q + 2];
+        const uint32_t e0 = lds[q + 4], e1 = lds[q + 5], e2 = lds[q + 6];
+        const uint32_t msk = mask32(b);
+        x0 = __builtin_amdgcn_alignbit(__builtin_amdgcn_alignbyte(e1, e0, m), __builtin_amdgcn_alignbyte(d1, d0, m), sh) & msk;
+        x1 = __builtin_amdgcn_alignbit(__builtin_amdgcn_alignbyte(e2, e1, m), __builtin_amdgcn_alignbyte(d2, d1, m), sh) & msk;
+    }
+    else
+    {
+        const uint32_t bp = p * 8u + 2u * t * b;
+        x0 = lds_bits64(lds, bp, b);
+        x1 = lds_bits64(lds, bp + b, b);
+    }
+}
+
+// Decode one 128v64 block at LDS byte s into lane t's values 2t, 2t+1.
+// Returns the consumed bytes (wave-uniform).  scr: 512 u64 per wave.
+__device__ __forceinline__ uint32_t decode_block128v64(const uint32_t * lds, uint32_t s, uint64_t * scr, uint32_t t, uint64_t & x0,
+                                                       uint64_t & x1)
+{
+    const uint32_t hw = uni(lds_u32(lds, s));
+    const uint32_t h = hw & 0xFFu, x1b = (hw >> 8) & 0xFFu;
+    if ((h & 0xC0u) == 0xC0u)
+    {
+        uint32_t b = h & 0x3Fu;
+        if (b == 63u)
+            b = 64u;
+        const uint64_t c = lds_u64(lds, s + 1u) & mask64d(b);
+        x0 = x1 = c;
+        return 1u + ((b + 7u) >> 3);
+    }
+    if ((h & 0x40u) == 0u)
+    {
+        const uint32_t hdr = (h & 0x80u) ? 2u : 1u;
+        const uint32_t bx = (h & 0x80u) ? min(x1b, 64u) : 0u;
+        uint32_t b = h & 0x7Fu;
+        if (b == 63u)
+            b = 64u;
+        b = min(b, 64u);
+        if (bx == 0u)
+        {
+            unpack128v64_lane(lds, s + hdr, b, t, x0, x1);
+            return hdr + 16u * b;
+        }
+        // 128-bit bitmap at s+2: lane t's bits 2t, 2t+1 sit in dword t>>4;
+        // rank = popcount of the dwords before (lanes 0,16,32,48 each bring
+        // one dword into a wave scan) + the bits below 2t in its own dword.
+        const uint32_t w = lds_u32(lds, s + 2u + 4u * (t >> 4));
+        const uint32_t sh = (2u * t) & 31u;
+        const uint32_t my = (w >> sh) & 3u;
+        const uint32_t pcd = __builtin_popcount(w);
+        const uint32_t incl = wave_incl_scan((t & 15u) == 0u ? pcd : 0u);
+        const uint32_t before = incl - pcd + __builtin_popcount(w & ((1u << sh) - 1u));
+        const uint32_t xn = uni(__builtin_amdgcn_readlane(incl, 63));
+        const uint32_t xs = s + 18u;
+        const uint32_t xbytes = (xn * bx + 7u) >> 3;
+        unpack128v64_lane(lds, xs + xbytes, b, t, x0, x1);
+        const uint64_t ex0 = lds_bits64(lds, xs * 8u + before * bx, bx);
+        const uint64_t ex1 = lds_bits64(lds, xs * 8u + (before + (my & 1u)) * bx, bx);
+        x0 |= (my & 1u) ? shl64(ex0, b) : 0ull;
+        x1 |= (my & 2u) ? shl64(ex1, b) : 0ull;
+        return 18u + xbytes + 16u * b;
+    }
+    uint32_t b = h & 0x3Fu;
+    if (b == 63u)
+        b = 64u;
+    unpack128v64_lane(lds, s + 2u, b, t, x0, x1);
+    const uint32_t end = vbyte_exceptions_g<true>(lds, s + 2u + 16u * b, x1b, scr, scr + 256, t);
+    x0 |= shl64(scr[2u * t], b);
+    x1 |= shl64(scr[2u * t + 1u], b);
+    return end - s;
+}
+
+// Delta-1 over the block (applyDelta1 of p4D1Dec128v64): inclusive scan of
+// v + 1 from start, mod 2^64.  Returns the block's last value.
+__device__ __forceinline__ uint64_t delta1_128v64(uint64_t & x0, uint64_t & x1, uint64_t start)
+{
+    const uint64_t a0 = x0 + 1u, a1 = a0 + x1 + 1u;
+    const uint64_t incl = wave_incl_scan64(a1);
+    const uint64_t base = start + incl - a1;
+    x0 = base + a0;
+    x1 = base + a1;
+    return start + readlane_u64(incl, 63);
+}
+
+template <uint32_t NB, bool D1>
+__global__ __launch_bounds__(256, 4) void k_dec128v64w(const uint8_t * __restrict in, uint64_t in_bytes,
+                                                       const uint64_t * __restrict off, uint64_t nunits,
+                                                       uint64_t * __restrict out, const uint64_t * __restrict starts,
+                                                       unsigned long long * __restrict err)
+{
+    constexpr uint32_t kRun = 16, NC = 3;
+    __shared__ uint32_t slots[4][kSlot64 / 4];
+    __shared__ uint64_t scratch[4][512];
+    const uint32_t t = threadIdx.x & 63u;
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    uint32_t * slot = slots[wv];
+    uint64_t * scr = scratch[wv];
+    const uint64_t in_base = reinterpret_cast<uint64_t>(in);
+    const uint64_t first = (static_cast<uint64_t>(blockIdx.x) * 4u + wv) * kRun;
+    if (first >= nunits)
+        return;
+    const uint32_t n = static_cast<uint32_t>(min_u64(kRun, nunits - first));
+
+    const bool valid = t < n;
+    const uint64_t unit = first + t;
+    const uint64_t o = valid ? off[unit] : 0ull;
+    const uint64_t e = valid ? off[unit + 1u] : 0ull;
+    RunPlaneT<kSlot64> P;
+    P.init(in_base, in_base + in_bytes, o, e, valid);
+    const uint64_t startv = (D1 && valid) ? starts[unit] : 0ull;
+    uint64_t badmask = 0u;
+    uint64_t * const out_run = out + first * (128u * NB);
+
+    auto consume = [&](const Chunk & c, uint32_t jj) {
+        const uint32_t ctl = P.stage(c, jj, slot, t);
+        uint32_t s = (ctl >> kCtlShift) & 15u;
+        const uint32_t s0 = s;
+        uint64_t carry = D1 ? readlane_u64(startv, jj) : 0ull;
+#pragma unroll
+        for (uint32_t u = 0; u < NB; ++u)
+        {
+            uint64_t x0, x1;
+            s += decode_block128v64(slot, s, scr, t, x0, x1);
+            if constexpr (D1)
+                carry = delta1_128v64(x0, x1, carry);
+            typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+            __builtin_nontemporal_store(u64x2{x0, x1}, reinterpret_cast<u64x2 *>(out_run + (jj * NB + u) * 128u) + t);
+            wave_lds_sync();
+        }
+        if (s - s0 != rl(P.len, jj))
+            badmask |= 1ull << jj;
+    };
+
+    Chunk C[NC];
+#pragma unroll
+    for (uint32_t u = 0; u + 1 < NC; ++u)
+        P.template issue<0>(C[u], u, t);
+    bool more = true;
+    for (uint32_t j = 0; more; j += NC)
+    {
+#pragma unroll
+        for (uint32_t u = 0; u < NC; ++u)
+        {
+            if (more)
+            {
+                P.template issue<0>(C[(u + NC - 1) % NC], j + u + NC - 1, t);
+                consume(C[u], j + u);
+                more = j + u + 1 < n;
+            }
+        }
+    }
+    if (err != nullptr && t == 0 && badmask != 0u)
+        atomicMin(err, static_cast<unsigned long long>(first + __builtin_ctzll(badmask)));
+}
+
+} // namespace tpf::dev
+
+namespace tpf
+{
+
+// fmt 128v64 (nb = 1) or 256v64 (nb = 2), n == 128 * nb values per unit.
+hipError_t launch_dec128v64(uint32_t nb, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nunits,
+                            uint64_t * out, const uint64_t * starts, unsigned long long * err, hipStream_t s)
+{
+    if (nunits == 0)
+        return hipSuccess;
+    const uint32_t grid = static_cast<uint32_t>((nunits + 63u) / 64u);
+    if (nb == 2u)
+    {
+        if (starts)
+            hipLaunchKernelGGL((dev::k_dec128v64w<2, true>), dim3(grid), dim3(256), 0, s, in, in_bytes, off, nunits, out, starts, err);
+        else
+            hipLaunchKernelGGL((dev::k_dec128v64w<2, false>), dim3(grid), dim3(256), 0, s, in, in_bytes, off, nunits, out, starts, err);
+    }
+    else
+    {
+        if (starts)
+            hipLaunchKernelGGL((dev::k_dec128v64w<1, true>), dim3(grid), dim3(256), 0, s, in, in_bytes, off, nunits, out, starts, err);
+        else
+            hipLaunchKernelGGL((dev::k_dec128v64w<1, false>), dim3(grid), dim3(256), 0, s, in, in_bytes, off, nunits, out, starts, err);
+    }
+    return hipGetLastError();
+}
+
+} // namespace tpf

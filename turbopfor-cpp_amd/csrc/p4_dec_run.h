@@ -50,7 +50,8 @@ __device__ __forceinline__ void st16(u32x4 * p, const u32x4 & v)
 // computed once in VALU and fetched per block with v_readlane.  The scalar
 // unit is shared by the CU's four SIMDs; per-block 64-bit address arithmetic
 // on it was the measured limiter before this layout.
-struct RunPlane
+template <uint32_t SLOT>
+struct RunPlaneT
 {
     uint32_t ctl;        // kCtl* bits
     uint32_t len;        // expected byte length (0xFFFFFFFF: implausible offsets)
@@ -62,8 +63,8 @@ struct RunPlane
     {
         const uint64_t ab = in_base + o;
         const uint64_t cb = ab & ~15ull;
-        span = valid ? static_cast<uint32_t>(min_u64(sub_sat(in_base + e, cb), kSlotBytes - 64)) : 0u;
-        avail = valid ? static_cast<uint32_t>(min_u64(sub_sat(in_end, cb), kSlotBytes)) : 0u;
+        span = valid ? static_cast<uint32_t>(min_u64(sub_sat(in_base + e, cb), SLOT - 64)) : 0u;
+        avail = valid ? static_cast<uint32_t>(min_u64(sub_sat(in_end, cb), SLOT)) : 0u;
         const bool slow = valid && (span > 2048u || span + 16u > avail);
         ctl = (slow ? 0u : span) | ((static_cast<uint32_t>(ab) & 15u) << kCtlShift) | (slow ? kCtlSlow : 0u)
             | (!slow && span > 1024u ? kCtlTwo : 0u);
@@ -80,7 +81,7 @@ struct RunPlane
     {
         const uint32_t cw = rl(ctl, jj);
         const uint64_t base = (static_cast<uint64_t>(rl(cbhi, jj)) << 32) | rl(cblo, jj);
-        const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(base), kSlotBytes);
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(base), SLOT);
         const uint32_t fspan = cw & kCtlSpan;
         c.a = ld16<POL>(rs, 16u * t < fspan ? 16u * t : 0x80000000u);
         c.b = ld16<POL>(rs, 1024u + 16u * t < fspan ? 1024u + 16u * t : 0x80000000u);
@@ -95,7 +96,7 @@ struct RunPlane
             reinterpret_cast<u32x4 *>(slot)[64 + t] = c.b;
         if (cw & kCtlSlow)
         {
-            // rare: > 2 KB blocks or the chunk straddling the end of the stream
+            // rare: > 2 KB units or the chunk straddling the end of the stream
             // (a raw buffer load that crosses num_records returns 0)
             const uint32_t sp = rl(span, jj), av = rl(avail, jj);
             const uint64_t base = (static_cast<uint64_t>(rl(cbhi, jj)) << 32) | rl(cblo, jj);
@@ -108,5 +109,7 @@ struct RunPlane
         return cw;
     }
 };
+
+using RunPlane = RunPlaneT<kSlotBytes>;
 
 } // namespace tpf::dev

@@ -287,10 +287,12 @@ hipError_t launch_dec_generic(int fmt, const uint8_t * in, uint64_t in_bytes, co
             return dec_fmt<dev::Fmt::V256, false>(in, in_bytes, off, nblocks, n, out, starts, err, s);
         case FMT_64:
             return dec_fmt<dev::Fmt::H64, false>(in, in_bytes, off, nblocks, n, out, starts, err, s);
-        case FMT_128V64:
-            return dec_fmt<dev::Fmt::V128X64, false>(in, in_bytes, off, nblocks, n, out, starts, err, s);
+        case FMT_128V64: // run-pipelined kernel, p4_dec256v64.hip (generic one-block-per-wave: 263 vs 468 G int64/s)
+            return launch_dec128v64(1, in, in_bytes, off, nblocks, static_cast<uint64_t *>(out),
+                                    static_cast<const uint64_t *>(starts), err, s);
         case FMT_256V64:
-            return dec_fmt<dev::Fmt::V128X64, true>(in, in_bytes, off, nblocks, n, out, starts, err, s);
+            return launch_dec128v64(2, in, in_bytes, off, nblocks, static_cast<uint64_t *>(out),
+                                    static_cast<const uint64_t *>(starts), err, s);
         default:
             return hipErrorInvalidValue;
     }

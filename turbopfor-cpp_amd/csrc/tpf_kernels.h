@@ -42,6 +42,9 @@ hipError_t launch_d1chain_sums(const uint8_t * in, uint64_t in_bytes, const uint
 hipError_t launch_d1chain_decode(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * out,
                                  const uint32_t * incl, uint32_t base, unsigned long long * err, hipStream_t stream);
 
+hipError_t launch_dec128v64(uint32_t nb, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nunits,
+                            uint64_t * out, const uint64_t * starts, unsigned long long * err, hipStream_t s);
+
 size_t enc256v32_workspace(uint64_t nblocks);
 hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, bool d1,
                             uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t stream);
