@@ -159,7 +159,6 @@ __global__ __launch_bounds__(256) void k_enc256v32_write(const uint32_t * __rest
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
     uint32_t * img = img_all[wv];
-    const uint8_t * ib = reinterpret_cast<const uint8_t *>(img);
     EncRun R;
     if (!R.init(in, nblocks, wv))
         return;
@@ -185,38 +184,7 @@ __global__ __launch_bounds__(256) void k_enc256v32_write(const uint32_t * __rest
         wave_lds_sync();
         const uint32_t sb = emit_block256(img, val_all[wv], P, v, t);
         wave_lds_sync();
-        // copy out: global dword i (from the aligned a0) holds block bytes
-        // [4i - phase, 4i - phase + 4) = image bytes [dl + 4i, dl + 4i + 4)
-        const uint32_t phase = static_cast<uint32_t>(dst & 3u);
-        const uint32_t dl = sb - phase; // 1..7
-        const uint32_t qs = dl >> 2, bs = dl & 3u;
-        uint32_t * const a0 = reinterpret_cast<uint32_t *>(dst & ~3ull);
-        const uint32_t end = phase + size;
-        const uint32_t nd = (end + 3u) >> 2;
-        const bool inside = dst + size <= cap_end;
-        const uint32_t lo_full = phase ? 1u : 0u;
-        const uint32_t hi_full = (end & 3u) ? nd - 1u : nd;
-        if (inside)
-            for (uint32_t d = lo_full + t; d < hi_full; d += 64u)
-                a0[d] = __builtin_amdgcn_alignbyte(img[d + qs + 1u], img[d + qs], bs);
-        // partial edge dwords (shared with the neighbouring blocks) byte by
-        // byte, lanes 0-3 the first dword and 4-7 the last, one store; a block
-        // crossing out_cap entirely byte by byte
-        if (inside)
-        {
-            const uint32_t d = t < 4u ? 0u : nd - 1u;
-            const uint32_t bi = 4u * d + (t & 3u); // byte index from a0
-            const bool edge = t < 4u ? (phase != 0u || ((end & 3u) != 0u && nd == 1u))
-                                     : (t < 8u && nd > 1u && (end & 3u) != 0u);
-            if (edge && bi >= phase && bi < end)
-                reinterpret_cast<uint8_t *>(a0)[bi] = ib[dl + bi];
-        }
-        else
-        {
-            for (uint32_t bi = phase + t; bi < end; bi += 64u)
-                if (reinterpret_cast<uint64_t>(reinterpret_cast<uint8_t *>(a0) + bi) < cap_end)
-                    reinterpret_cast<uint8_t *>(a0)[bi] = ib[dl + bi];
-        }
+        copy_out_image(img, sb, dst, size, cap_end, t);
         wave_lds_sync();
     });
 }

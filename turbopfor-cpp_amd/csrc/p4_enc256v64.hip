@@ -1,0 +1,473 @@
+// p4_enc256v64.hip -- batch encode of 128v64 / 256v64 P4 blocks (p4Enc128v64,
+// p4Enc256v64 and their D1 variants; reference
+// src/scalar/p4enc128v64_scalar.cpp:51-224, p4enc256v64_scalar.cpp:15-30,
+// p4d1enc256v64_scalar.cpp) on gfx950.
+//
+// Same three launches as the 256v32 encoder (p4_enc256v32.hip): plan (cost
+// model + exact sizes) -> exclusive scan of unit sizes -> write.  A unit is
+// one reference call: one 128v64 block (NB = 1) or the two 128v64 blocks of a
+// 256v64 call (NB = 2).  Lane t owns values 2t, 2t+1 of each 128-value block:
+// one 16-byte load per lane per block, the layout of k_dec128v64w.
+// Each block is built in its own LDS image whose dword phase puts the base
+// payload on a dword (a 256v64 unit's second block starts at an arbitrary
+// byte), then copied out (copy_out_image, p4_enc32.h).
+#include <hipcub/hipcub.hpp>
+
+#include "p4_generic.h"
+#include "tpf_kernels.h"
+
+namespace tpf::dev
+{
+
+constexpr uint32_t kEnc64Run = 16;    // units per wave run
+constexpr uint32_t kEnc64NC = 3;      // units in flight per wave
+constexpr uint32_t kImg64U32 = 592;   // block image: 4..7 lead + block (<= 2150 B) + slack
+constexpr uint32_t kVal64U32 = 128;   // staged low halves (b <= 32 base packing)
+
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+struct Chunk64
+{
+    u32x4 a, b; // blocks 0 and 1 of the unit, lane t = values 2t, 2t+1
+};
+
+__device__ __forceinline__ void split2(const u32x4 & c, uint64_t & x0, uint64_t & x1)
+{
+    x0 = (static_cast<uint64_t>(c.y) << 32) | c.x;
+    x1 = (static_cast<uint64_t>(c.w) << 32) | c.z;
+}
+
+// 64-bit lane shuffle up by one (ds_bpermute twice)
+__device__ __forceinline__ uint64_t shfl_up1_64(uint64_t x)
+{
+    const uint32_t lo = static_cast<uint32_t>(__shfl_up(static_cast<int>(static_cast<uint32_t>(x)), 1, 64));
+    const uint32_t hi = static_cast<uint32_t>(__shfl_up(static_cast<int>(static_cast<uint32_t>(x >> 32)), 1, 64));
+    return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// deltaEnc1 (p4_scalar_internal.h:711-719) over one 128-value block:
+// d[e] = x[e] - x[e-1] - 1 with x[-1] = prev.
+__device__ __forceinline__ void delta_encode64(uint64_t & x0, uint64_t & x1, uint64_t prev, uint32_t t)
+{
+    uint64_t p = shfl_up1_64(x1);
+    if (t == 0)
+        p = prev;
+    const uint64_t d0 = x0 - p - 1u, d1 = x1 - x0 - 1u;
+    x0 = d0;
+    x1 = d1;
+}
+
+// Plan word of one block: b | bx << 7 | xn << 14 | raw << 22 (23 bits).
+__device__ __forceinline__ uint32_t plan64_word(const PlanG & P) { return P.b | (P.bx << 7) | (P.xn << 14) | (P.raw << 22); }
+
+__device__ __forceinline__ PlanG plan64_unword(uint32_t w, uint32_t size)
+{
+    PlanG P;
+    P.b = w & 0x7Fu;
+    P.bx = (w >> 7) & 0x7Fu;
+    P.xn = (w >> 14) & 0xFFu;
+    P.raw = (w >> 22) & 1u;
+    P.size = size;
+    return P;
+}
+
+__device__ __forceinline__ PlanG plan_block128v64(uint64_t x0, uint64_t x1, uint32_t * hist, uint32_t t)
+{
+    const uint64_t v[4] = {x0, x1, 0ull, 0ull}; // element order is irrelevant to the cost model
+    return plan_block_g<Fmt::V128X64>(v, 128u, hist, t);
+}
+
+// OR cnt (0..2) consecutive nb-bit (<= 64) values a, b into the image's bit
+// stream at `bit` (five dwords at most).
+__device__ __forceinline__ void or_pair64(uint32_t * img, uint32_t bit, uint64_t a, uint64_t b, uint32_t cnt, uint32_t nb)
+{
+    if (cnt == 0u || nb == 0u)
+        return;
+    const uint64_t m = mask64d(nb);
+    a &= m;
+    b = cnt > 1u ? (b & m) : 0ull;
+    const uint64_t lo = a | shl64(b, nb);
+    const uint64_t hi = nb == 0u ? 0ull : (nb >= 64u ? b : (b >> (64u - nb)));
+    const uint32_t sh = bit & 31u, q = bit >> 5;
+    const uint32_t d0 = static_cast<uint32_t>(lo), d1 = static_cast<uint32_t>(lo >> 32);
+    const uint32_t d2 = static_cast<uint32_t>(hi), d3 = static_cast<uint32_t>(hi >> 32);
+    uint32_t w[5];
+    w[0] = d0 << sh;
+    w[1] = sh ? __builtin_amdgcn_alignbit(d1, d0, 32u - sh) : d1;
+    w[2] = sh ? __builtin_amdgcn_alignbit(d2, d1, 32u - sh) : d2;
+    w[3] = sh ? __builtin_amdgcn_alignbit(d3, d2, 32u - sh) : d3;
+    w[4] = sh ? (d3 >> (32u - sh)) : 0u;
+    const uint32_t nw = (sh + cnt * nb + 31u) >> 5;
+#pragma unroll
+    for (uint32_t i = 0; i < 5; ++i)
+        if (i < nw && w[i] != 0u)
+            atomicOr(&img[q + i], w[i]);
+}
+
+// Interleave the low 16 bits of x to the even bit positions of a dword.
+__device__ __forceinline__ uint32_t spread16(uint32_t x)
+{
+    x &= 0xFFFFu;
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    return x;
+}
+
+// vbPut64 encoding (p4_scalar_internal.cpp:447-476) of x at image byte pos.
+__device__ __forceinline__ void vbput64_img(uint32_t * img, uint32_t pos, uint64_t x)
+{
+    const uint32_t bp = pos * 8u;
+    if (x < 152u)
+        or_bits(img, bp, static_cast<uint32_t>(x), 8);
+    else if (x < 16536u)
+    {
+        const uint32_t d = static_cast<uint32_t>(x) - 152u;
+        or_bits(img, bp, (0x98u + (d >> 8)) | ((d & 0xFFu) << 8), 16);
+    }
+    else if (x < 2113688u)
+    {
+        const uint32_t d = static_cast<uint32_t>(x) - 16536u;
+        or_bits(img, bp, (0xD8u + (d >> 16)) | ((d & 0xFFFFu) << 8), 24);
+    }
+    else
+    {
+        const uint32_t nb = (bw64d(x) + 7u) >> 3;
+        or_bits(img, bp, 0xF8u + (nb - 3u), 8);
+        or_bits64(img, bp + 8u, x, 8u * nb);
+    }
+}
+
+// Build one 128v64 block (p4Enc128v64 = writeHeader64 + p4Enc128v64Payload)
+// in the zeroed image; returns sb, the image byte of the block's first byte.
+__device__ __forceinline__ uint32_t emit_block128v64(uint32_t * img, uint32_t * val, const PlanG & P, uint64_t x0, uint64_t x1,
+                                                     uint32_t t)
+{
+    uint8_t * const ib = reinterpret_cast<uint8_t *>(img);
+    const uint32_t b = P.b;
+    const uint32_t bh = b >= 64u ? 63u : b; // header stores 64 as 63
+    if (P.bx == 66u)
+    {
+        // constant block: ceil(b/8) bytes of element 0
+        const uint64_t c = readlane_u64(x0, 0) & mask64d(b);
+        if (t == 0)
+            ib[4] = static_cast<uint8_t>(0xC0u | bh);
+        if (t < ((b + 7u) >> 3))
+            ib[5 + t] = static_cast<uint8_t>(c >> (8u * t));
+        return 4u;
+    }
+    const uint64_t m = mask64d(b);
+    const uint32_t xbytes = (P.bx != 0u && P.bx <= 64u) ? ((P.xn * P.bx + 7u) >> 3) : 0u;
+    const uint32_t po = P.bx == 0u ? 1u : (P.bx <= 64u ? 18u + xbytes : 2u); // payload offset in the block
+    const uint32_t sb = 4u + ((4u - (po & 3u)) & 3u);
+    const uint32_t pw = (sb + po) >> 2;
+    const uint64_t m0 = x0 & m, m1 = x1 & m;
+    const uint32_t f0 = x0 > m, f1 = x1 > m;
+    // headers
+    if (t == 0)
+    {
+        if (P.bx == 0u)
+            ib[sb] = static_cast<uint8_t>(bh);
+        else if (P.bx <= 64u)
+        {
+            ib[sb] = static_cast<uint8_t>(0x80u | bh);
+            ib[sb + 1u] = static_cast<uint8_t>(P.bx);
+        }
+        else
+        {
+            ib[sb] = static_cast<uint8_t>(0x40u | bh);
+            ib[sb + 1u] = static_cast<uint8_t>(P.xn);
+        }
+    }
+    // base payload (bitpack128v64Scalar, bitpack128v64_scalar.cpp:38-104)
+    if (b != 0u && b <= 32u)
+    {
+        // 128v32 layout of the pair-swapped low halves: column l, group g holds
+        // element (4g + l) ^ 2.  Lane t < 32 ORs a run of groups 4r..4r+3 of
+        // column l = t >> 3 (so at most 8 lanes share a dword).
+        reinterpret_cast<uint64_t *>(val)[t] = (static_cast<uint64_t>(static_cast<uint32_t>(m1)) << 32) | static_cast<uint32_t>(m0);
+        wave_lds_sync();
+        if (t < 32u)
+        {
+            const uint32_t l = t >> 3, r = t & 7u;
+            uint32_t x[4];
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i)
+                x[i] = val[(4u * (4u * r + i) + l) ^ 2u];
+            or_run(img, pw + l, 4u, 4u * r * b, x, 4u, b, run_maxw(4u, b));
+        }
+    }
+    else if (b > 32u)
+    {
+        // horizontal 64-bit stream: values 2t, 2t+1 are consecutive
+        or_pair64(img, pw * 32u + 2u * t * b, m0, m1, 2u, b);
+    }
+    if (P.bx == 0u)
+        return sb;
+    const uint64_t B0 = __ballot(f0), B1 = __ballot(f1);
+    const uint32_t cnt = f0 + f1;
+    const uint32_t before = static_cast<uint32_t>(__builtin_popcountll(B0 & lanemask_lt()) + __builtin_popcountll(B1 & lanemask_lt()));
+    const uint64_t e0 = b >= 64u ? 0ull : (x0 >> b), e1 = b >= 64u ? 0ull : (x1 >> b);
+    const uint64_t xa = f0 ? e0 : e1; // this lane's exceptions, compacted
+    if (P.bx <= 64u)
+    {
+        // [0x80|b][bx][bitmap 16 B][xn * bx bits][base]
+        if (t < 4u)
+        {
+            const uint32_t piece = spread16(static_cast<uint32_t>(B0 >> (16u * t))) | (spread16(static_cast<uint32_t>(B1 >> (16u * t))) << 1);
+            or_bits(img, (sb + 2u) * 8u + 32u * t, piece, 32);
+        }
+        or_pair64(img, (sb + 18u) * 8u + before * P.bx, xa, e1, cnt, P.bx);
+        return sb;
+    }
+    // vbyte: [0x40|b][xn][base 16b][V][positions]
+    const uint32_t v0 = sb + 2u + 16u * b;
+    if (P.raw)
+    {
+        if (t == 0)
+            or_bits(img, v0 * 8u, 0xFFu, 8);
+        if (f0)
+        {
+            or_bits64(img, (v0 + 1u + 8u * before) * 8u, e0, 64);
+            or_bits(img, (v0 + 1u + 8u * P.xn + before) * 8u, 2u * t, 8);
+        }
+        if (f1)
+        {
+            or_bits64(img, (v0 + 1u + 8u * (before + f0)) * 8u, e1, 64);
+            or_bits(img, (v0 + 1u + 8u * P.xn + before + f0) * 8u, 2u * t + 1u, 8);
+        }
+        return sb;
+    }
+    const uint32_t l0 = f0 ? vblen64(e0) : 0u, l1 = f1 ? vblen64(e1) : 0u;
+    const uint32_t lincl = wave_incl_scan(l0 + l1);
+    const uint32_t vtot = __builtin_amdgcn_readlane(lincl, 63);
+    const uint32_t pos = v0 + lincl - l0 - l1;
+    if (f0)
+    {
+        vbput64_img(img, pos, e0);
+        or_bits(img, (v0 + vtot + before) * 8u, 2u * t, 8);
+    }
+    if (f1)
+    {
+        vbput64_img(img, pos + l0, e1);
+        or_bits(img, (v0 + vtot + before + f0) * 8u, 2u * t + 1u, 8);
+    }
+    return sb;
+}
+
+// A wave's run of up to kEnc64Run consecutive units (NB blocks of 128 u64).
+template <uint32_t NB>
+struct EncRun64
+{
+    uint64_t first;
+    uint32_t n;
+    __amdgpu_buffer_rsrc_t rs;
+
+    __device__ __forceinline__ bool init(const uint64_t * in, uint64_t nunits, uint32_t wv)
+    {
+        first = (static_cast<uint64_t>(blockIdx.x) * 4u + wv) * kEnc64Run;
+        if (first >= nunits)
+            return false;
+        n = static_cast<uint32_t>(min_u64(kEnc64Run, nunits - first));
+        rs = make_rsrc(in + first * (128u * NB), n * 1024u * NB);
+        return true;
+    }
+
+    __device__ __forceinline__ void load(Chunk64 & c, uint32_t jj, uint32_t t) const
+    {
+        c.a = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(jj * 1024u * NB + 16u * t), 0, 0);
+        if constexpr (NB == 2)
+            c.b = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(jj * 2048u + 1024u + 16u * t), 0, 0);
+    }
+
+    // value preceding unit first+t (lanes t < n): the given starts, or for one
+    // chained list the last value of the previous unit
+    __device__ __forceinline__ uint64_t start_lane(const uint64_t * in, const uint64_t * starts, uint64_t start0, uint32_t t) const
+    {
+        if (t >= n)
+            return 0ull;
+        const uint64_t u = first + t;
+        if (starts)
+            return starts[u];
+        return u == 0 ? start0 : in[u * (128u * NB) - 1u];
+    }
+
+    // body(chunk, jj) for jj = 0..n-1 with kEnc64NC units in flight
+    template <class Body>
+    __device__ __forceinline__ void walk(uint32_t t, Body && body) const
+    {
+        Chunk64 C[kEnc64NC];
+#pragma unroll
+        for (uint32_t u = 0; u + 1 < kEnc64NC; ++u)
+            load(C[u], u, t);
+        bool more = true;
+        for (uint32_t j = 0; more; j += kEnc64NC)
+        {
+#pragma unroll
+            for (uint32_t u = 0; u < kEnc64NC; ++u)
+            {
+                if (more)
+                {
+                    load(C[(u + kEnc64NC - 1) % kEnc64NC], j + u + kEnc64NC - 1, t);
+                    body(C[u], j + u);
+                    more = j + u + 1 < n;
+                }
+            }
+        }
+    }
+};
+
+// The unit's blocks as (x0, x1) pairs after optional delta coding.
+template <uint32_t NB, bool D1>
+__device__ __forceinline__ void unit_values(const Chunk64 & c, uint64_t start, uint32_t t, uint64_t (&x)[2][2])
+{
+    split2(c.a, x[0][0], x[0][1]);
+    if constexpr (NB == 2)
+        split2(c.b, x[1][0], x[1][1]);
+    if constexpr (D1)
+    {
+        const uint64_t last0 = readlane_u64(x[0][1], 63); // element 127, before coding
+        delta_encode64(x[0][0], x[0][1], start, t);
+        if constexpr (NB == 2)
+            delta_encode64(x[1][0], x[1][1], last0, t);
+    }
+}
+
+template <uint32_t NB, bool D1>
+__global__ __launch_bounds__(256) void k_enc128v64_plan(const uint64_t * __restrict in, uint64_t nunits,
+                                                        const uint64_t * __restrict starts, uint64_t start0,
+                                                        uint64_t * __restrict sizes, uint64_t * __restrict plan)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t hist[4][kPlanGHistU32];
+    const uint32_t t = threadIdx.x & 63u;
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        sizes[nunits] = 0; // exclusive scan over nunits+1 entries yields the total
+    EncRun64<NB> R;
+    if (!R.init(in, nunits, wv))
+        return;
+    const uint64_t stv = D1 ? R.start_lane(in, starts, start0, t) : 0ull;
+    uint32_t szv = 0u;
+    uint64_t pwv = 0ull; // lane j: unit first+j
+    R.walk(t, [&](const Chunk64 & c, uint32_t jj) {
+        uint64_t x[2][2];
+        unit_values<NB, D1>(c, D1 ? readlane_u64(stv, jj) : 0ull, t, x);
+        const PlanG P0 = plan_block128v64(x[0][0], x[0][1], hist[wv], t);
+        uint32_t size = P0.size;
+        uint64_t w = plan64_word(P0);
+        if constexpr (NB == 2)
+        {
+            const PlanG P1 = plan_block128v64(x[1][0], x[1][1], hist[wv], t);
+            size += P1.size;
+            w |= (static_cast<uint64_t>(plan64_word(P1)) << 23) | (static_cast<uint64_t>(P0.size) << 46);
+        }
+        szv = t == jj ? size : szv;
+        pwv = t == jj ? w : pwv;
+    });
+    if (t < R.n)
+    {
+        sizes[R.first + t] = szv;
+        plan[R.first + t] = pwv;
+    }
+}
+
+template <uint32_t NB, bool D1>
+__global__ __launch_bounds__(256) void k_enc128v64_write(const uint64_t * __restrict in, uint64_t nunits,
+                                                         const uint64_t * __restrict starts, uint64_t start0,
+                                                         const uint64_t * __restrict off, const uint64_t * __restrict plan,
+                                                         uint8_t * __restrict out, uint64_t out_cap)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t img_all[4][kImg64U32];
+    __shared__ __attribute__((aligned(16))) uint32_t val_all[4][kVal64U32];
+    const uint32_t t = threadIdx.x & 63u;
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    uint32_t * img = img_all[wv];
+    EncRun64<NB> R;
+    if (!R.init(in, nunits, wv))
+        return;
+    const uint64_t stv = D1 ? R.start_lane(in, starts, start0, t) : 0ull;
+    const uint64_t ov = t < R.n ? off[R.first + t] : 0ull;
+    const uint64_t ev = t < R.n ? off[R.first + t + 1u] : 0ull;
+    const uint64_t pwv = t < R.n ? plan[R.first + t] : 0ull;
+    const uint64_t out_base = reinterpret_cast<uint64_t>(out);
+    const uint64_t cap_end = out_base + out_cap;
+    R.walk(t, [&](const Chunk64 & c, uint32_t jj) {
+        uint64_t x[2][2];
+        unit_values<NB, D1>(c, D1 ? readlane_u64(stv, jj) : 0ull, t, x);
+        const uint64_t o = readlane_u64(ov, jj);
+        const uint32_t usize = static_cast<uint32_t>(readlane_u64(ev, jj) - o);
+        const uint64_t w = readlane_u64(pwv, jj);
+        const uint32_t size0 = NB == 2 ? static_cast<uint32_t>(w >> 46) : usize;
+#pragma unroll
+        for (uint32_t u = 0; u < NB; ++u)
+        {
+            const uint32_t size = u == 0 ? size0 : usize - size0;
+            const PlanG P = plan64_unword(static_cast<uint32_t>(w >> (23u * u)) & 0x7FFFFFu, size);
+            const uint64_t dst = out_base + o + (u == 0 ? 0u : size0);
+#pragma unroll
+            for (uint32_t i = 0; i < 3; ++i)
+                if (t + 64u * i < kImg64U32 / 4u)
+                    reinterpret_cast<u32x4 *>(img)[t + 64u * i] = u32x4{0u, 0u, 0u, 0u};
+            wave_lds_sync();
+            const uint32_t sb = emit_block128v64(img, val_all[wv], P, x[u][0], x[u][1], t);
+            wave_lds_sync();
+            copy_out_image(img, sb, dst, size, cap_end, t);
+            wave_lds_sync();
+        }
+    });
+}
+
+} // namespace tpf::dev
+
+namespace tpf
+{
+
+size_t enc128v64_workspace(uint64_t nunits)
+{
+    size_t scan_bytes = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, static_cast<uint64_t *>(nullptr),
+                                           static_cast<int>(std::min<uint64_t>(nunits + 1, 0x7FFFFFFF)));
+    return ((nunits * 8u + 255u) & ~size_t(255)) + scan_bytes + 256;
+}
+
+namespace
+{
+template <uint32_t NB, bool D1>
+hipError_t enc64_launch(const uint64_t * in, uint64_t nunits, const uint64_t * starts, uint64_t start0, uint8_t * out,
+                        uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t s)
+{
+    auto * plan = static_cast<uint64_t *>(ws);
+    const size_t plan_bytes = (nunits * 8u + 255u) & ~size_t(255);
+    void * scan_tmp = static_cast<uint8_t *>(ws) + plan_bytes;
+    size_t scan_bytes = ws_bytes > plan_bytes ? ws_bytes - plan_bytes : 0;
+    const uint64_t per_wg = 4ull * dev::kEnc64Run;
+    const uint32_t grid = static_cast<uint32_t>((nunits + per_wg - 1) / per_wg);
+    hipLaunchKernelGGL((dev::k_enc128v64_plan<NB, D1>), dim3(grid), dim3(256), 0, s, in, nunits, starts, start0, off, plan);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return e;
+    e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, off, static_cast<int>(nunits + 1), s);
+    if (e != hipSuccess)
+        return e;
+    hipLaunchKernelGGL((dev::k_enc128v64_write<NB, D1>), dim3(grid), dim3(256), 0, s, in, nunits, starts, start0, off, plan, out,
+                       out_cap);
+    return hipGetLastError();
+}
+} // namespace
+
+hipError_t launch_enc128v64(uint32_t nb, const uint64_t * in, uint64_t nunits, bool d1, const uint64_t * starts, uint64_t start0,
+                            uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t s)
+{
+    if (nunits == 0)
+        return hipMemsetAsync(off, 0, sizeof(uint64_t), s);
+    if (nunits + 1 > 0x7FFFFFFFull)
+        return hipErrorInvalidValue;
+    if (nb == 2u)
+        return d1 ? enc64_launch<2, true>(in, nunits, starts, start0, out, out_cap, off, ws, ws_bytes, s)
+                  : enc64_launch<2, false>(in, nunits, starts, start0, out, out_cap, off, ws, ws_bytes, s);
+    return d1 ? enc64_launch<1, true>(in, nunits, starts, start0, out, out_cap, off, ws, ws_bytes, s)
+              : enc64_launch<1, false>(in, nunits, starts, start0, out, out_cap, off, ws, ws_bytes, s);
+}
+
+} // namespace tpf

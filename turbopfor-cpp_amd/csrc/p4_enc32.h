@@ -351,4 +351,41 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
     return sb;
 }
 
+// Copy a block built in an LDS image (block byte 0 at image byte sb, 4..7)
+// to dst (any alignment): global dword i from the aligned a0 holds block
+// bytes [4i - phase, 4i - phase + 4) = image bytes [dl + 4i, dl + 4i + 4).
+// Full dwords with dword stores; the two edge dwords shared with the
+// neighbouring blocks byte by byte (lanes 0-3 the first dword, 4-7 the last,
+// one store); a block crossing cap_end entirely byte by byte.
+__device__ __forceinline__ void copy_out_image(const uint32_t * img, uint32_t sb, uint64_t dst, uint32_t size, uint64_t cap_end,
+                                               uint32_t t)
+{
+    const uint8_t * ib = reinterpret_cast<const uint8_t *>(img);
+    const uint32_t phase = static_cast<uint32_t>(dst & 3u);
+    const uint32_t dl = sb - phase; // 1..7
+    const uint32_t qs = dl >> 2, bs = dl & 3u;
+    uint32_t * const a0 = reinterpret_cast<uint32_t *>(dst & ~3ull);
+    const uint32_t end = phase + size;
+    const uint32_t nd = (end + 3u) >> 2;
+    const bool inside = dst + size <= cap_end;
+    const uint32_t lo_full = phase ? 1u : 0u;
+    const uint32_t hi_full = (end & 3u) ? nd - 1u : nd;
+    if (inside)
+    {
+        for (uint32_t d = lo_full + t; d < hi_full; d += 64u)
+            a0[d] = __builtin_amdgcn_alignbyte(img[d + qs + 1u], img[d + qs], bs);
+        const uint32_t d = t < 4u ? 0u : nd - 1u;
+        const uint32_t bi = 4u * d + (t & 3u); // byte index from a0
+        const bool edge = t < 4u ? (phase != 0u || ((end & 3u) != 0u && nd == 1u)) : (t < 8u && nd > 1u && (end & 3u) != 0u);
+        if (edge && bi >= phase && bi < end)
+            reinterpret_cast<uint8_t *>(a0)[bi] = ib[dl + bi];
+    }
+    else
+    {
+        for (uint32_t bi = phase + t; bi < end; bi += 64u)
+            if (reinterpret_cast<uint64_t>(reinterpret_cast<uint8_t *>(a0) + bi) < cap_end)
+                reinterpret_cast<uint8_t *>(a0)[bi] = ib[dl + bi];
+    }
+}
+
 } // namespace tpf::dev

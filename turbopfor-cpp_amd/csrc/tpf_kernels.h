@@ -45,6 +45,10 @@ hipError_t launch_d1chain_decode(const uint8_t * in, uint64_t in_bytes, const ui
 hipError_t launch_dec128v64(uint32_t nb, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nunits,
                             uint64_t * out, const uint64_t * starts, unsigned long long * err, hipStream_t s);
 
+size_t enc128v64_workspace(uint64_t nunits);
+hipError_t launch_enc128v64(uint32_t nb, const uint64_t * in, uint64_t nunits, bool d1, const uint64_t * starts, uint64_t start0,
+                            uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t s);
+
 size_t enc256v32_workspace(uint64_t nblocks);
 hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, bool d1,
                             uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t stream);
