@@ -73,10 +73,9 @@ struct BitmapInfo
     uint32_t xn;     // total (wave-uniform)
 };
 
-__device__ __forceinline__ BitmapInfo read_bitmap256(const uint32_t * lds, uint32_t bm_pos, uint32_t t)
+__device__ __forceinline__ BitmapInfo read_bitmap256(uint32_t w, uint32_t t)
 {
     BitmapInfo bi;
-    const uint32_t w = lds_u32(lds, bm_pos + 4u * (t >> 3));
     const uint32_t sh = 4u * (t & 7u);
     bi.my = (w >> sh) & 0xFu;
     const uint32_t pcd = __builtin_popcount(w);
@@ -209,10 +208,15 @@ __device__ __forceinline__ uint32_t vbyte_exceptions(const uint32_t * lds, uint3
 }
 
 // Decode one 256v32 block at LDS byte s.  Returns consumed bytes (uniform).
-// The header byte and the byte after it (bx / xn) arrive with one read.
-__device__ __forceinline__ uint32_t decode_block256v32(const uint32_t * lds, uint32_t s, uint32_t * scr, uint32_t t, u32x4 & v)
+// hw: the block's first 4 bytes (header byte, bx / xn byte), wave-uniform,
+// taken by the caller from the load registers so the mode is known without
+// an LDS round trip.  The lane's bitmap dword is read before the mode
+// branch (a harmless in-slot read for other modes) so that a bitmap block
+// needs one LDS round trip before its unpack instead of two.
+__device__ __forceinline__ uint32_t decode_block256v32(const uint32_t * lds, uint32_t s, uint32_t hw, uint32_t * scr, uint32_t t,
+                                                       u32x4 & v)
 {
-    const uint32_t hw = uni(lds_u32(lds, s));
+    const uint32_t wbm = lds_u32(lds, s + 2u + 4u * (t >> 3));
     const uint32_t h = hw & 0xFFu, x1 = (hw >> 8) & 0xFFu;
     if ((h & 0xC0u) == 0xC0u)
     {
@@ -233,7 +237,7 @@ __device__ __forceinline__ uint32_t decode_block256v32(const uint32_t * lds, uin
             v = unpack256v32_lane(lds, s + hdr, b, t);
             return hdr + 32u * b;
         }
-        const BitmapInfo bi = read_bitmap256(lds, s + 2u, t);
+        const BitmapInfo bi = read_bitmap256(wbm, t);
         const uint32_t xs = s + 34u;
         const uint32_t xbytes = (bi.xn * bx + 7u) >> 3;
         v = unpack256v32_lane(lds, xs + xbytes, b, t);

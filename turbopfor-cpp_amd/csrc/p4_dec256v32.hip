@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
         }
         else
         {
-            used = decode_block256v32(slot, (ctl >> kCtlShift) & 15u, scr, t, v);
+            used = decode_block256v32(slot, (ctl >> kCtlShift) & 15u, P.head(c, ctl, slot), scr, t, v);
             if constexpr (SM == StartMode::PerBlock || SM == StartMode::Prefix)
                 apply_delta1_256(v, rl(startv, jj));
             st16<POL>(reinterpret_cast<u32x4 *>(out_run + jj * stride * 256u) + t, v);

@@ -87,6 +87,21 @@ struct RunPlaneT
         c.b = ld16<POL>(rs, 1024u + 16u * t < fspan ? 1024u + 16u * t : 0x80000000u);
     }
 
+    // First 4 bytes of block jj (wave-uniform), from the load registers:
+    // lane 0 holds chunk bytes 0..15, lane 1 bytes 16..31.  Slow-path blocks
+    // (staged by guarded loads) read them from the slot instead.
+    __device__ __forceinline__ uint32_t head(const Chunk & c, uint32_t cw, const uint32_t * slot) const
+    {
+        const uint32_t s = (cw >> kCtlShift) & 15u;
+        if (cw & kCtlSlow)
+            return uni(lds_u32(slot, s));
+        const uint32_t a0 = rl(c.a.x, 0), a1 = rl(c.a.y, 0), a2 = rl(c.a.z, 0), a3 = rl(c.a.w, 0), a4 = rl(c.a.x, 1);
+        const uint32_t k = s >> 2;
+        const uint32_t lo = k == 0 ? a0 : k == 1 ? a1 : k == 2 ? a2 : a3;
+        const uint32_t hi = k == 0 ? a1 : k == 1 ? a2 : k == 2 ? a3 : a4;
+        return uni(__builtin_amdgcn_alignbyte(hi, lo, s & 3u));
+    }
+
     // Write block jj's chunk into the wave's LDS slot; returns its ctl word.
     __device__ __forceinline__ uint32_t stage(const Chunk & c, uint32_t jj, uint32_t * slot, uint32_t t) const
     {

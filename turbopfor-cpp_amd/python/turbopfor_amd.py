@@ -13,7 +13,8 @@ import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libturbopfor_amd.so")
+# TPF_LIB: load another build of the library (A/B measurements only)
+LIB_PATH = os.environ.get("TPF_LIB") or os.path.join(PKG_DIR, "lib", "libturbopfor_amd.so")
 
 _lib = None
 
