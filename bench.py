@@ -466,10 +466,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist_on = world > 1
+    # Rehearsal of the multi-rank path on a one-GPU box (never the measured
+    # configuration): TPF_BENCH_BACKEND=gloo TPF_BENCH_SAME_GPU=1 puts every
+    # rank on cuda:0 and carries the collectives over gloo.
+    backend = os.environ.get("TPF_BENCH_BACKEND", "nccl")
+    if os.environ.get("TPF_BENCH_SAME_GPU") == "1":
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
     if dist_on:
-        torch.distributed.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=dev)
+        else:
+            torch.distributed.init_process_group(backend)
     T = Timer(dist_on, dev)
     if args.workload == "c2":
         res = run_c2(args, world, rank, dev, T)
