@@ -171,20 +171,20 @@ __global__ __launch_bounds__(256) void k_enc256v32_write(const uint32_t * __rest
     const uint32_t olo = static_cast<uint32_t>(ov), ohi = static_cast<uint32_t>(ov >> 32);
     const uint64_t out_base = reinterpret_cast<uint64_t>(out);
     const uint64_t cap_end = out_base + out_cap;
+    zero_image(img, kImgU32 / 4u, t);
+    wave_lds_sync();
     R.walk(t, [&](u32x4 v, uint32_t jj) {
         if constexpr (D1)
             v = delta_encode(v, rl32(stv, jj), t);
         const uint32_t size = rl32(szv, jj);
         const Plan32 P = unplan(rl32(pwv, jj), size);
         const uint64_t dst = out_base + ((static_cast<uint64_t>(rl32(ohi, jj)) << 32) | rl32(olo, jj));
-#pragma unroll
-        for (uint32_t i = 0; i < 3; ++i)
-            if (t + 64u * i < kImgU32 / 4u)
-                reinterpret_cast<u32x4 *>(img)[t + 64u * i] = u32x4{0u, 0u, 0u, 0u};
-        wave_lds_sync();
         const uint32_t sb = emit_block256(img, val_all[wv], P, v, t);
         wave_lds_sync();
-        copy_out_image(img, sb, dst, size, cap_end, t);
+        copy_out_image16(img, sb, dst, size, cap_end, t);
+        wave_lds_sync();
+        // only [0, sb + size) can be non-zero: clear it for the next block
+        zero_image(img, min((sb + size + 15u) >> 4, kImgU32 / 4u), t);
         wave_lds_sync();
     });
 }

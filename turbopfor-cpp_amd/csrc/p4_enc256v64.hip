@@ -10,7 +10,7 @@
 // one 16-byte load per lane per block, the layout of k_dec128v64w.
 // Each block is built in its own LDS image whose dword phase puts the base
 // payload on a dword (a 256v64 unit's second block starts at an arbitrary
-// byte), then copied out (copy_out_image, p4_enc32.h).
+// byte), then copied out (copy_out_image16, p4_enc32.h).
 #include <hipcub/hipcub.hpp>
 
 #include "p4_generic.h"
@@ -152,15 +152,15 @@ __device__ __forceinline__ uint32_t emit_block128v64(uint32_t * img, uint32_t * 
         // constant block: ceil(b/8) bytes of element 0
         const uint64_t c = readlane_u64(x0, 0) & mask64d(b);
         if (t == 0)
-            ib[4] = static_cast<uint8_t>(0xC0u | bh);
+            ib[kImgLead] = static_cast<uint8_t>(0xC0u | bh);
         if (t < ((b + 7u) >> 3))
-            ib[5 + t] = static_cast<uint8_t>(c >> (8u * t));
-        return 4u;
+            ib[kImgLead + 1u + t] = static_cast<uint8_t>(c >> (8u * t));
+        return kImgLead;
     }
     const uint64_t m = mask64d(b);
     const uint32_t xbytes = (P.bx != 0u && P.bx <= 64u) ? ((P.xn * P.bx + 7u) >> 3) : 0u;
     const uint32_t po = P.bx == 0u ? 1u : (P.bx <= 64u ? 18u + xbytes : 2u); // payload offset in the block
-    const uint32_t sb = 4u + ((4u - (po & 3u)) & 3u);
+    const uint32_t sb = kImgLead + ((4u - (po & 3u)) & 3u);
     const uint32_t pw = (sb + po) >> 2;
     const uint64_t m0 = x0 & m, m1 = x1 & m;
     const uint32_t f0 = x0 > m, f1 = x1 > m;
@@ -392,6 +392,8 @@ __global__ __launch_bounds__(256) void k_enc128v64_write(const uint64_t * __rest
     const uint64_t pwv = t < R.n ? plan[R.first + t] : 0ull;
     const uint64_t out_base = reinterpret_cast<uint64_t>(out);
     const uint64_t cap_end = out_base + out_cap;
+    zero_image(img, kImg64U32 / 4u, t);
+    wave_lds_sync();
     R.walk(t, [&](const Chunk64 & c, uint32_t jj) {
         uint64_t x[2][2];
         unit_values<NB, D1>(c, D1 ? readlane_u64(stv, jj) : 0ull, t, x);
@@ -405,14 +407,11 @@ __global__ __launch_bounds__(256) void k_enc128v64_write(const uint64_t * __rest
             const uint32_t size = u == 0 ? size0 : usize - size0;
             const PlanG P = plan64_unword(static_cast<uint32_t>(w >> (23u * u)) & 0x7FFFFFu, size);
             const uint64_t dst = out_base + o + (u == 0 ? 0u : size0);
-#pragma unroll
-            for (uint32_t i = 0; i < 3; ++i)
-                if (t + 64u * i < kImg64U32 / 4u)
-                    reinterpret_cast<u32x4 *>(img)[t + 64u * i] = u32x4{0u, 0u, 0u, 0u};
-            wave_lds_sync();
             const uint32_t sb = emit_block128v64(img, val_all[wv], P, x[u][0], x[u][1], t);
             wave_lds_sync();
-            copy_out_image(img, sb, dst, size, cap_end, t);
+            copy_out_image16(img, sb, dst, size, cap_end, t);
+            wave_lds_sync();
+            zero_image(img, min((sb + size + 15u) >> 4, kImg64U32 / 4u), t);
             wave_lds_sync();
         }
     });

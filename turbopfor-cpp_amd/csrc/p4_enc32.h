@@ -147,8 +147,8 @@ __device__ __forceinline__ void or_bits(uint32_t * img, uint32_t bp, uint32_t va
 
 // ---- block image construction (write pass) --------------------------------
 // The image of one block is built in LDS so that its base payload starts on
-// a dword: the block starts at image byte sb = 4 + s0, s0 in [0,3] chosen
-// from the payload offset, and the copy-out shifts by bytes (v_alignbyte).
+// a dword: the block starts at image byte sb = kImgLead + s0, s0 in [0,3]
+// chosen from the payload offset, and the copy-out shifts by bytes (v_alignbyte).
 // Each lane ORs RUNS of up to four consecutive values of one bit stream
 // (concatenated in registers first) into the image, so a dword receives few
 // atomic ORs: for the base payload lane t = 8l + r takes column l's groups
@@ -159,6 +159,10 @@ __device__ __forceinline__ void or_bits(uint32_t * img, uint32_t bp, uint32_t va
 // was slower still (dependent LDS reads, 7.4 ms per 10M blocks).
 
 constexpr uint32_t kEncValU32 = 256; // staged masked base values, element order
+// Block images start at byte kImgLead..kImgLead+3 (the payload lands on a
+// dword); the 16-byte lead lets copy_out_image16 address the first chunk
+// before the block without going below the image.
+constexpr uint32_t kImgLead = 20;
 
 // OR cnt (<= 4) consecutive nb-bit values x[] (each < 2^nb) into a bit stream
 // at stream bit `bit`; stream dword i lives at img[dw0 + stride * i].  maxw:
@@ -227,15 +231,15 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
         // constant block (p4enc256v32_scalar.cpp:183-190): ceil(b/8) value bytes
         const uint32_t x = v.x & mask32(b);
         if (t == 0)
-            ib[4] = static_cast<uint8_t>(0xC0u | b);
+            ib[kImgLead] = static_cast<uint8_t>(0xC0u | b);
         if (t < ((b + 7u) >> 3))
-            ib[5 + t] = static_cast<uint8_t>(x >> (8u * t));
-        return 4u;
+            ib[kImgLead + 1u + t] = static_cast<uint8_t>(x >> (8u * t));
+        return kImgLead;
     }
     const uint32_t m = mask32(b);
     const uint32_t xbytes = P.bx <= 32u ? ((P.xn * P.bx + 7u) >> 3) : 0u;
     const uint32_t po = P.bx == 0u ? 1u : (P.bx <= 32u ? 34u + xbytes : 2u); // payload offset in the block
-    const uint32_t sb = 4u + ((4u - (po & 3u)) & 3u);
+    const uint32_t sb = kImgLead + ((4u - (po & 3u)) & 3u);
     const uint32_t pw = (sb + po) >> 2;
     reinterpret_cast<u32x4 *>(val)[t] = u32x4{v.x & m, v.y & m, v.z & m, v.w & m};
     if (P.bx == 0u)
@@ -351,40 +355,56 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
     return sb;
 }
 
-// Copy a block built in an LDS image (block byte 0 at image byte sb, 4..7)
-// to dst (any alignment): global dword i from the aligned a0 holds block
-// bytes [4i - phase, 4i - phase + 4) = image bytes [dl + 4i, dl + 4i + 4).
-// Full dwords with dword stores; the two edge dwords shared with the
-// neighbouring blocks byte by byte (lanes 0-3 the first dword, 4-7 the last,
-// one store); a block crossing cap_end entirely byte by byte.
-__device__ __forceinline__ void copy_out_image(const uint32_t * img, uint32_t sb, uint64_t dst, uint32_t size, uint64_t cap_end,
-                                               uint32_t t)
+// Copy a block built in an LDS image (block byte 0 at image byte sb >= 16)
+// to dst (any alignment) with 16-byte stores: global chunk k of a16 = dst & ~15
+// holds block bytes [16k - ph, 16k - ph + 16), ph = dst & 15, i.e. image
+// bytes from base + 16k, base = sb - ph.  A full chunk costs 5 aligned
+// ds_read_b32 + 4 v_alignbyte + one global_store_dwordx4 per lane (a 600-byte
+// block: one store instruction instead of three dword stores); the partial
+// first and last chunks, shared with the neighbouring blocks, are written
+// byte by byte (lanes 0-15 and 16-31); a block crossing cap_end entirely byte
+// by byte.
+// Zero image u32x4 slots [0, n16) (a whole image: kImgU32 / 4).
+__device__ __forceinline__ void zero_image(uint32_t * img, uint32_t n16, uint32_t t)
+{
+    for (uint32_t i = t; i < n16; i += 64u)
+        reinterpret_cast<u32x4 *>(img)[i] = u32x4{0u, 0u, 0u, 0u};
+}
+
+__device__ __forceinline__ void copy_out_image16(const uint32_t * img, uint32_t sb, uint64_t dst, uint32_t size, uint64_t cap_end,
+                                                 uint32_t t)
 {
     const uint8_t * ib = reinterpret_cast<const uint8_t *>(img);
-    const uint32_t phase = static_cast<uint32_t>(dst & 3u);
-    const uint32_t dl = sb - phase; // 1..7
-    const uint32_t qs = dl >> 2, bs = dl & 3u;
-    uint32_t * const a0 = reinterpret_cast<uint32_t *>(dst & ~3ull);
-    const uint32_t end = phase + size;
-    const uint32_t nd = (end + 3u) >> 2;
-    const bool inside = dst + size <= cap_end;
-    const uint32_t lo_full = phase ? 1u : 0u;
-    const uint32_t hi_full = (end & 3u) ? nd - 1u : nd;
-    if (inside)
+    const uint32_t ph = static_cast<uint32_t>(dst & 15u);
+    const uint32_t base = sb - ph;
+    uint8_t * const a16 = reinterpret_cast<uint8_t *>(dst & ~15ull);
+    const uint32_t end = ph + size;
+    if (dst + size <= cap_end)
     {
-        for (uint32_t d = lo_full + t; d < hi_full; d += 64u)
-            a0[d] = __builtin_amdgcn_alignbyte(img[d + qs + 1u], img[d + qs], bs);
-        const uint32_t d = t < 4u ? 0u : nd - 1u;
-        const uint32_t bi = 4u * d + (t & 3u); // byte index from a0
-        const bool edge = t < 4u ? (phase != 0u || ((end & 3u) != 0u && nd == 1u)) : (t < 8u && nd > 1u && (end & 3u) != 0u);
-        if (edge && bi >= phase && bi < end)
-            reinterpret_cast<uint8_t *>(a0)[bi] = ib[dl + bi];
+        const bool first_partial = ph != 0u || end < 16u;
+        const uint32_t k_lo = first_partial ? 1u : 0u;
+        const uint32_t k_hi = end >> 4; // chunks below k_hi end inside the block
+        const uint32_t bs = base & 3u;
+        for (uint32_t k = k_lo + t; k < k_hi; k += 64u)
+        {
+            const uint32_t q = (base >> 2) + 4u * k;
+            const uint32_t w0 = img[q], w1 = img[q + 1], w2 = img[q + 2], w3 = img[q + 3], w4 = img[q + 4];
+            *reinterpret_cast<u32x4 *>(a16 + 16u * k) =
+                u32x4{__builtin_amdgcn_alignbyte(w1, w0, bs), __builtin_amdgcn_alignbyte(w2, w1, bs),
+                      __builtin_amdgcn_alignbyte(w3, w2, bs), __builtin_amdgcn_alignbyte(w4, w3, bs)};
+        }
+        const uint32_t last = (end - 1u) >> 4; // chunk holding the block's last byte
+        const uint32_t k = t < 16u ? 0u : last;
+        const bool edge = t < 16u ? first_partial : (t < 32u && last > 0u && (end & 15u) != 0u);
+        const uint32_t gi = 16u * k + (t & 15u); // byte index from a16
+        if (edge && gi >= ph && gi < end)
+            a16[gi] = ib[base + gi];
     }
     else
     {
-        for (uint32_t bi = phase + t; bi < end; bi += 64u)
-            if (reinterpret_cast<uint64_t>(reinterpret_cast<uint8_t *>(a0) + bi) < cap_end)
-                reinterpret_cast<uint8_t *>(a0)[bi] = ib[dl + bi];
+        for (uint32_t gi = ph + t; gi < end; gi += 64u)
+            if (reinterpret_cast<uint64_t>(a16 + gi) < cap_end)
+                a16[gi] = ib[base + gi];
     }
 }
 
