@@ -81,11 +81,12 @@ __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist
         return c < 64u ? x : 0u;
     };
     const uint32_t vbacc = at(t + 7u) + 2u * at(t + 15u) + 3u * at(t + 19u) + 4u * at(t + 25u);
-    const uint32_t a = cnt, bsum = cnt + vbacc;
-    const uint32_t pa = wave_incl_scan(a), pb = wave_incl_scan(bsum);
-    const uint32_t ta = __builtin_amdgcn_readlane(pa, 63), tb = __builtin_amdgcn_readlane(pb, 63);
-    const uint32_t ec = ta - pa;    // sum_{c > t} cnt[c]
-    const uint32_t vbsum = tb - pb; // sum_{c > t} (cnt[c] + vbacc[c])
+    // both suffix sums in ONE scan: cnt <= 256 in the low half, cnt + vbacc
+    // <= 5*256 in the high half (no carry between the halves)
+    const uint32_t pab = wave_incl_scan(cnt | ((cnt + vbacc) << 16));
+    const uint32_t tab = __builtin_amdgcn_readlane(pab, 63);
+    const uint32_t ec = (tab & 0xFFFFu) - (pab & 0xFFFFu); // sum_{c > t} cnt[c]
+    const uint32_t vbsum = (tab >> 16) - (pab >> 16);     // sum_{c > t} (cnt[c] + vbacc[c])
     uint32_t key = 0xFFFFFFFFu;
     if (t < maxb)
     {
@@ -113,7 +114,15 @@ __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist
     }
     const uint32_t b = P.b;
     const uint32_t m = mask32(b);
-    const uint32_t xn = wave_sum((v.x > m) + (v.y > m) + (v.z > m) + (v.w > m));
+    // exception count (low half) and, for vbyte, their vbyte bytes (high
+    // half, <= 5*256) in one reduction
+    uint32_t cl = (v.x > m) + (v.y > m) + (v.z > m) + (v.w > m);
+    if (kind != 0u)
+        cl |= ((v.x > m ? vblen32(v.x >> b) : 0u) + (v.y > m ? vblen32(v.y >> b) : 0u) + (v.z > m ? vblen32(v.z >> b) : 0u)
+               + (v.w > m ? vblen32(v.w >> b) : 0u))
+            << 16;
+    const uint32_t tot = wave_sum(cl);
+    const uint32_t xn = tot & 0xFFFFu;
     P.xn = xn;
     if (kind == 0u)
     {
@@ -124,9 +133,7 @@ __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist
     else
     {
         P.bx = 33;
-        const uint32_t sl = (v.x > m ? vblen32(v.x >> b) : 0u) + (v.y > m ? vblen32(v.y >> b) : 0u)
-            + (v.z > m ? vblen32(v.z >> b) : 0u) + (v.w > m ? vblen32(v.w >> b) : 0u);
-        const uint32_t sumlen = wave_sum(sl);
+        const uint32_t sumlen = tot >> 16;
         P.raw = (sumlen + 32u > 4u * xn) ? 1u : 0u;
         const uint32_t vsize = P.raw ? 1u + 4u * xn : sumlen;
         P.size = 2u + 32u * b + vsize + xn;

@@ -420,10 +420,11 @@ __device__ __forceinline__ PlanG plan_block_g(const typename FmtTraits<F>::T v[4
         return c < 64u ? x : (c == 64u ? cnt64 : 0u);
     };
     const uint32_t vbacc = at(t + 7u) + 2u * at(t + 15u) + 3u * at(t + 19u) + 4u * at(t + 25u);
-    const uint32_t pa = wave_incl_scan(cnt), pb = wave_incl_scan(cnt + vbacc);
-    const uint32_t ta = __builtin_amdgcn_readlane(pa, 63), tb = __builtin_amdgcn_readlane(pb, 63);
-    const uint32_t ec = ta - pa + cnt64;
-    const uint32_t vbsum = tb - pb + cnt64;
+    // both suffix sums in one scan (cnt <= 256 low half, cnt + vbacc <= 11*256 high half)
+    const uint32_t pab = wave_incl_scan(cnt | ((cnt + vbacc) << 16));
+    const uint32_t tab = __builtin_amdgcn_readlane(pab, 63);
+    const uint32_t ec = (tab & 0xFFFFu) - (pab & 0xFFFFu) + cnt64;
+    const uint32_t vbsum = (tab >> 16) - (pab >> 16) + cnt64;
     uint32_t key = 0xFFFFFFFFu;
     const uint32_t bmp = pad8d(n);
     if (t < maxb)
@@ -458,7 +459,8 @@ __device__ __forceinline__ PlanG plan_block_g(const typename FmtTraits<F>::T v[4
             const uint64_t ex = static_cast<uint64_t>(v[j]) >> b;
             sl += wide ? vblen64(ex) : vblen32(static_cast<uint32_t>(ex));
         }
-    const uint32_t xn = wave_sum(xc);
+    const uint32_t xs_tot = wave_sum(xc | (sl << 16)); // count | vbyte bytes (<= 9*256)
+    const uint32_t xn = xs_tot & 0xFFFFu;
     P.b = b;
     P.xn = xn;
     if ((kmin & 1u) == 0u)
@@ -469,7 +471,7 @@ __device__ __forceinline__ PlanG plan_block_g(const typename FmtTraits<F>::T v[4
     else
     {
         P.bx = W + 1u;
-        const uint32_t sumlen = wave_sum(sl);
+        const uint32_t sumlen = xs_tot >> 16;
         constexpr uint32_t ES = W / 8u;
         P.raw = (sumlen + 32u > ES * xn) ? 1u : 0u;
         P.size = 2u + base_bytes<F>(NE, b) + (P.raw ? 1u + ES * xn : sumlen) + xn;
