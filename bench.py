@@ -14,7 +14,8 @@ Other workloads (--workload, one JSON line each, for DESIGN.md):
   c3chain the same list decoded as ONE chained list (only start0 given)
   c4      p4Enc256v32 + p4Dec256v32 round trip (0/5/10/25% exceptions) and
           the 256v64 round trip (bw 1..64 with exceptions above bit 32)
---e2e adds the host-memory rate (pinned H2D + decode + D2H, tpf_host_dec).
+--e2e adds the host-memory rates (pinned H2D + decode + D2H, tpf_host_dec; and
+      the encode trip, tpf_host_enc).
 
 Multi-GPU (torchrun, one process per GPU): every rank owns its own shard
 (weak scaling); the decode needs no collective.  RCCL carries the barrier,
@@ -321,25 +322,50 @@ def run_c2(args, world, rank, dev, T):
 
 
 def measure_e2e(packed, offs, nb, vals):
-    """Host-memory rate: pinned packed bytes + offsets in, pinned values out,
-    chunked H2D / decode / D2H overlap inside tpf_host_dec."""
+    """Host-memory rates (the north star's end-to-end number): pinned packed
+    bytes + offsets in, pinned values out, tpf_host_dec (chunk uploads by
+    SDMA overlapped with the decode and the download of the previous chunk);
+    and the reverse trip, tpf_host_enc, from pinned values to a pinned
+    stream + offsets."""
     L = tpf.lib()
     L.tpf_host_dec.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
                                ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]
+    L.tpf_host_enc.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_int,
+                               ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
     h_in = packed.cpu().pin_memory()
     h_off = offs.cpu().pin_memory()
     h_out = torch.empty((nb, 256), dtype=torch.int32).pin_memory()
-    L.tpf_host_dec(2, h_in.data_ptr(), h_in.numel(), h_off.data_ptr(), nb, 256, h_out.data_ptr(), None)
     reps = 3
-    t0 = time.perf_counter()
-    for _ in range(reps):
+
+    def dec():
         rc = L.tpf_host_dec(2, h_in.data_ptr(), h_in.numel(), h_off.data_ptr(), nb, 256, h_out.data_ptr(), None)
         assert rc == 0, L.tpf_last_error()
+
+    dec()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dec()
     dt = (time.perf_counter() - t0) / reps
     ok = bool(torch.equal(h_out, vals.cpu()))
     r = {"G_int32_per_s": round(nb * 256 / dt / 1e9, 2), "s_per_pass": round(dt, 4),
          "pcie_GBps_in_plus_out": round((h_in.numel() + nb * 1032) / dt / 1e9, 2), "verified": ok}
-    log(f"[e2e] host-pinned decode: {r}")
+    cap = h_in.numel() + 64
+    h_pk = torch.empty(cap, dtype=torch.uint8).pin_memory()
+    h_po = torch.empty(nb + 1, dtype=torch.int64).pin_memory()
+
+    def enc():
+        rc = L.tpf_host_enc(2, h_out.data_ptr(), nb, 256, 0, None, 0, h_pk.data_ptr(), cap, h_po.data_ptr())
+        assert rc == 0, L.tpf_last_error()
+
+    enc()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        enc()
+    dt = (time.perf_counter() - t0) / reps
+    ok_e = bool(torch.equal(h_po, h_off.view(torch.int64)) and torch.equal(h_pk[: h_in.numel()], h_in))
+    r["enc"] = {"G_int32_per_s": round(nb * 256 / dt / 1e9, 2), "s_per_pass": round(dt, 4),
+                "pcie_GBps_in_plus_out": round((h_in.numel() + nb * 1032) / dt / 1e9, 2), "verified": ok_e}
+    log(f"[e2e] host-pinned decode/encode: {r}")
     return r
 
 

@@ -65,15 +65,18 @@ int64_t tpf_scan_offsets(int fmt, const uint8_t *in, uint64_t in_bytes, unsigned
 /* ---- host-memory streams (end-to-end path) ----------------
  * Decode / encode nblocks blocks whose bytes and values live in HOST memory:
  * the work is split into chunks that are copied to HBM, processed and copied
- * back with H2D / kernel / D2H overlapped on separate HIP streams.  Host
- * buffers allocated with hipHostMalloc (or registered) give full PCIe rate;
- * pageable buffers are registered for the duration of the call.
+ * back, the upload of chunk k+1 overlapping the kernel and the download of
+ * chunk k (a copy stream and a kernel stream).  Host buffers allocated with
+ * hipHostMalloc (or registered) give full PCIe rate; pageable buffers are
+ * registered (and mapped) for the duration of the call.  Staging buffers and
+ * streams are pooled per device across calls; tpf_host_release() frees them.
  * h_off may be NULL for decode (offsets are scanned with tpf_scan_offsets).
  * Value arrays use the unit strides documented in turbopfor_gpu.h. */
 int tpf_host_dec(int fmt, const uint8_t *h_in, uint64_t in_bytes, const uint64_t *h_off, uint64_t nblocks, unsigned n,
                  void *h_vals, const void *h_starts);
 int tpf_host_enc(int fmt, const void *h_vals, uint64_t nblocks, unsigned n, int d1, const void *h_starts, uint64_t start0,
                  uint8_t *h_out, uint64_t out_cap, uint64_t *h_off);
+void tpf_host_release(void);
 
 #ifdef __cplusplus
 }

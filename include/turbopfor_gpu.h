@@ -122,6 +122,13 @@ int tpf_dec_batch(int fmt, const uint8_t *d_in, uint64_t in_bytes, const uint64_
 int tpf_enc_batch(int fmt, const void *d_vals, uint64_t nblocks, unsigned n, int d1, const void *d_starts, uint64_t start0,
                   uint8_t *d_out, uint64_t out_cap, uint64_t *d_off, void *d_ws, size_t ws_bytes, void *stream);
 
+/* ---- host pipeline utility ----------------------------------------------
+ * Copies `bytes` bytes with a kernel (16-byte non-temporal stores) instead of
+ * an SDMA engine; either side may be pinned/registered host memory, at any
+ * byte alignment.  The tpf_host_* pipelines use it for downloads under
+ * TPF_HOST_DOWN=kernel (SDMA is their default: faster on MI355X). */
+int tpf_copy_async(void *dst, const void *src, uint64_t bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -78,7 +78,12 @@ def test_reference_style_cpp_caller(tmp_path):
     assert res.stdout.startswith("ok:"), res.stdout
 
 
-def test_host_streams_vs_oracle():
+@pytest.mark.parametrize("chunk_bytes", [None, 1000 * 1024, 777 * 1024])
+def test_host_streams_vs_oracle(chunk_bytes, monkeypatch):
+    """Pageable numpy buffers (registered + mapped for the call); with small
+    chunks the pipeline runs many chunks through its 3 slots."""
+    if chunk_bytes:
+        monkeypatch.setenv("TPF_HOST_CHUNK_BYTES", str(chunk_bytes))
     L = capi()
     L.tpf_host_dec.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
                                ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]
@@ -111,3 +116,62 @@ def test_host_streams_vs_oracle():
                         starts.ctypes.data)
     assert rc == 0, L.tpf_last_error()
     np.testing.assert_array_equal(back2, vals)
+
+
+@pytest.mark.parametrize("down", ["sdma", "kernel"])
+def test_host_streams_pinned_torch(down, monkeypatch):
+    """Pinned (hipHostMalloc) torch buffers, odd destination phase.  down=sdma
+    (default): results come back by hipMemcpyAsync; down=kernel: decode
+    stores straight into host memory and encode copies its bytes out with the
+    copy kernel at whatever byte phase each chunk lands on."""
+    monkeypatch.setenv("TPF_HOST_CHUNK_BYTES", str(513 * 1024))
+    monkeypatch.setenv("TPF_HOST_DOWN", down)
+    L = capi()
+    L.tpf_host_dec.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                               ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]
+    L.tpf_host_enc.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_int,
+                               ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    blocks = np.concatenate([datagen.c2_blocks(1500, bw, 10, seed=9) for bw in (1, 5, 12, 20, 28, 32)])
+    exp_packed, exp_off = oracle_lib.enc256v32_batch(blocks)
+    nb = len(blocks)
+    h_vals = torch.from_numpy(blocks.view(np.int32)).pin_memory()
+    cap = nb * 1100 + 64
+    h_pk = torch.zeros(cap + 3, dtype=torch.uint8).pin_memory()
+    h_po = torch.zeros(nb + 1, dtype=torch.int64).pin_memory()
+    base = h_pk.data_ptr() + 3  # odd destination phase
+    assert L.tpf_host_enc(2, h_vals.data_ptr(), nb, 256, 0, None, 0, base, cap, h_po.data_ptr()) == 0, L.tpf_last_error()
+    np.testing.assert_array_equal(h_po.numpy().view(np.uint64), exp_off)
+    np.testing.assert_array_equal(h_pk.numpy()[3:3 + len(exp_packed)], exp_packed)
+    assert not h_pk.numpy()[:3].any() and not h_pk.numpy()[3 + len(exp_packed):].any()
+    h_back = torch.zeros_like(h_vals).pin_memory()
+    assert L.tpf_host_dec(2, base, len(exp_packed), h_po.data_ptr(), nb, 256, h_back.data_ptr(), None) == 0, \
+        L.tpf_last_error()
+    np.testing.assert_array_equal(h_back.numpy().view(np.uint32), blocks)
+
+
+def test_copy_async_phases():
+    """tpf_copy_async (the pipelines' download path): every source/destination
+    phase mod 16 class, lengths around the 16-byte vector edges, device ->
+    pinned host, pinned host -> device and device -> device."""
+    L = capi()
+    L.tpf_copy_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    rng = np.random.default_rng(3)
+    n = (1 << 20) + 64
+    src_h = torch.from_numpy(rng.integers(0, 256, n, dtype=np.uint8))
+    src_d = src_h.cuda()
+    src_p = src_h.pin_memory()
+    dst_d = torch.empty(n, dtype=torch.uint8, device="cuda")
+    dst_p = torch.empty(n, dtype=torch.uint8).pin_memory()
+    cases = [(sp, dp, ln) for sp in (0, 1, 3, 4, 8, 13) for dp in (0, 2, 5, 15)
+             for ln in (0, 1, 15, 16, 17, 31, 100, 4099)]
+    cases += [(7, 0, n - 64), (0, 0, n - 64), (4, 12, 65536 + 3)]
+    stream = torch.cuda.current_stream().cuda_stream
+    for sp, dp, ln in cases:
+        for src, dst in ((src_d, dst_p), (src_p, dst_d), (src_d, dst_d)):
+            dst.fill_(0xAB)
+            assert L.tpf_copy_async(dst.data_ptr() + dp, src.data_ptr() + sp, ln, stream) == 0, L.tpf_last_error()
+            torch.cuda.synchronize()
+            got = dst.cpu().numpy()
+            want = src_h.numpy()
+            np.testing.assert_array_equal(got[dp:dp + ln], want[sp:sp + ln], err_msg=f"{sp} {dp} {ln}")
+            assert (got[:dp] == 0xAB).all() and (got[dp + ln:dp + ln + 64] == 0xAB).all(), (sp, dp, ln)

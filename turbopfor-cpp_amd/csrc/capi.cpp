@@ -302,4 +302,14 @@ int tpf_enc_batch(int fmt, const void * d_vals, uint64_t nblocks, unsigned n, in
     return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_enc_batch");
 }
 
+int tpf_copy_async(void * dst, const void * src, uint64_t bytes, void * stream)
+{
+    if (int rc = check_device())
+        return rc;
+    if (bytes && (!dst || !src))
+        return fail(TPF_EINVAL, "tpf_copy_async: null pointer");
+    hipError_t e = tpf::launch_copy(dst, src, bytes, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_copy_async");
+}
+
 } // extern "C"

@@ -1,0 +1,89 @@
+// host_copy.hip -- copy kernel for the host pipelines.
+//
+// Moving decoded values (or encoded bytes) between HBM and pinned host memory
+// with a kernel instead of an SDMA engine (the host pipelines' A/B
+// alternative, TPF_HOST_DOWN=kernel: measured 54 GB/s to the host vs 57 GB/s
+// for SDMA, so SDMA stays the default).  Each lane moves 16-byte vectors with
+// non-temporal stores; the head/tail bytes that are not 16-byte aligned at
+// the destination go byte by byte.
+#include <hip/hip_runtime.h>
+
+#include "tpf_device.h"
+#include "tpf_kernels.h"
+
+namespace tpf::dev
+{
+
+// Destination-aligned copy: vector i covers dst[head + 16i, +16).  When the
+// source shares the destination's phase mod 16 it is read with 16-byte loads;
+// otherwise with five aligned dword loads and v_alignbyte (every dword read
+// holds at least one byte of the source range, so nothing outside the
+// source's pages is touched).  Edge bytes (head, tail) go one by one.
+template <bool kAligned>
+__global__ __launch_bounds__(256) void k_copy16(uint8_t * __restrict__ dst, const uint8_t * __restrict__ src, uint64_t head,
+                                                uint64_t nvec, uint64_t bytes)
+{
+    const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+    u32x4 * d = reinterpret_cast<u32x4 *>(dst + head);
+    if constexpr (kAligned)
+    {
+        const u32x4 * s = reinterpret_cast<const u32x4 *>(src + head);
+        for (uint64_t i = gid; i < nvec; i += stride)
+            __builtin_nontemporal_store(s[i], d + i);
+    }
+    else
+    {
+        const uintptr_t s0 = reinterpret_cast<uintptr_t>(src + head);
+        const uint32_t sh = static_cast<uint32_t>(s0 & 3u);
+        const uint32_t * w = reinterpret_cast<const uint32_t *>(s0 & ~uintptr_t(3));
+        for (uint64_t i = gid; i < nvec; i += stride)
+        {
+            const uint32_t * q = w + 4u * i;
+            const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+            u32x4 v{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                    __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
+            __builtin_nontemporal_store(v, d + i);
+        }
+    }
+    // unaligned head [0, head) and tail [head + 16 nvec, bytes)
+    const uint64_t tail0 = head + nvec * 16u;
+    const uint64_t nedge = head + (bytes - tail0);
+    for (uint64_t i = gid; i < nedge; i += stride)
+    {
+        const uint64_t p = i < head ? i : tail0 + (i - head);
+        dst[p] = src[p];
+    }
+}
+
+} // namespace tpf::dev
+
+namespace tpf
+{
+
+hipError_t launch_copy(void * dst, const void * src, uint64_t bytes, hipStream_t s)
+{
+    if (bytes == 0)
+        return hipSuccess;
+    const uintptr_t d = reinterpret_cast<uintptr_t>(dst), sp = reinterpret_cast<uintptr_t>(src);
+    uint64_t head = (16u - (d & 15u)) & 15u;
+    if (head > bytes)
+        head = bytes;
+    uint64_t nvec = (bytes - head) / 16u;
+    const bool aligned = ((d ^ sp) & 15u) == 0;
+    // the shifted reader loads one dword past each vector: keep the last
+    // vector only if that dword still holds source bytes
+    if (!aligned && nvec && (((sp + head + 16u * nvec) & 3u) == 0) && head + 16u * nvec == bytes)
+        --nvec;
+    const uint64_t want = (nvec + 32u + 255u) / 256u;
+    const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>(want, grid_cap(s, 4)));
+    if (aligned)
+        hipLaunchKernelGGL(dev::k_copy16<true>, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, static_cast<uint8_t *>(dst),
+                           static_cast<const uint8_t *>(src), head, nvec, bytes);
+    else
+        hipLaunchKernelGGL(dev::k_copy16<false>, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, static_cast<uint8_t *>(dst),
+                           static_cast<const uint8_t *>(src), head, nvec, bytes);
+    return hipGetLastError();
+}
+
+} // namespace tpf

@@ -1,12 +1,27 @@
 // host_stream.cpp -- end-to-end host-memory streams: blocks
-// and values live in host memory; chunks are copied to HBM, decoded/encoded
-// by the batched kernels and copied back, with H2D, kernels and D2H of
-// different chunks overlapped on kSets HIP streams (PCIe is full duplex, the
-// kernels run at HBM speed, so the PCIe links bound this path).
+// and values live in host memory; chunks are uploaded to HBM, decoded/encoded
+// by the batched kernels and the results brought back, with the upload of
+// chunk k+1 (copy stream, SDMA) overlapping the kernel and the download of
+// chunk k (kernel stream).  PCIe is full duplex and the kernels run at HBM
+// speed, so the PCIe link bounds this path.
+//
+// Downloads go by SDMA (hipMemcpyAsync on the kernel stream): an SDMA upload
+// and an SDMA download on two streams overlap on MI355X (82 GB/s combined vs
+// 57 GB/s one way, scripts/e2e_probe.py).  TPF_HOST_DOWN=kernel instead has
+// the decode kernel store straight into the mapped host array and encode
+// move its bytes with the copy kernel (host_copy.hip); measured 4-8% slower
+// (profiles/r1_v4_e2e_probe.txt), kept for A/B.
+//
+// The staging buffers, streams and events of a pipeline are pooled across
+// calls (per device): allocating ~200 MB of HBM and pinned offset staging per
+// call cost more than the transfers (8.4 -> 12.5 G int32/s end to end).
+// tpf_host_release() frees the pool.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -22,7 +37,24 @@ void set_last_error(const std::string & msg);
 namespace
 {
 
-constexpr int kSets = 3;
+constexpr int kSlots = 3;
+
+// chunk = this many bytes of values: small enough that the first upload (not
+// overlapped) is short, large enough to fill the GPU per launch.
+// TPF_HOST_CHUNK_BYTES overrides it (tests drive many chunks through small inputs).
+uint64_t chunk_value_bytes()
+{
+    if (const char * e = std::getenv("TPF_HOST_CHUNK_BYTES"))
+        if (const uint64_t v = std::strtoull(e, nullptr, 10))
+            return v;
+    return 64ull << 20;
+}
+
+bool sdma_down()
+{
+    const char * e = std::getenv("TPF_HOST_DOWN");
+    return !(e && std::strcmp(e, "kernel") == 0);
+}
 
 bool wide_fmt(int fmt) { return fmt == TPF_FMT_64 || fmt == TPF_FMT_128V64 || fmt == TPF_FMT_256V64; }
 
@@ -53,20 +85,41 @@ void hc(hipError_t e, const char * what)
         throw Err(TPF_EHIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-// Page-lock a host range for the duration of a call unless it already is.
+void tc(int rc)
+{
+    if (rc != TPF_OK)
+        throw Err(rc, tpf_last_error());
+}
+
+// Page-lock (and map) a host range for the duration of a call unless it
+// already is; d = the range's device address (nullptr if the device cannot
+// address it, e.g. registration failed).
 struct Pin
 {
     void * p = nullptr;
+    void * d = nullptr;
     Pin(const void * ptr, size_t bytes)
     {
         if (!ptr || !bytes)
             return;
         hipPointerAttribute_t a{};
         if (hipPointerGetAttributes(&a, ptr) == hipSuccess && a.type != hipMemoryTypeUnregistered)
+        {
+            if (a.type == hipMemoryTypeHost && a.devicePointer && a.hostPointer)
+                d = static_cast<uint8_t *>(a.devicePointer)
+                    + (static_cast<const uint8_t *>(ptr) - static_cast<const uint8_t *>(a.hostPointer));
             return;
+        }
         (void)hipGetLastError();
-        if (hipHostRegister(const_cast<void *>(ptr), bytes, hipHostRegisterDefault) == hipSuccess)
+        if (hipHostRegister(const_cast<void *>(ptr), bytes, hipHostRegisterMapped) == hipSuccess)
+        {
             p = const_cast<void *>(ptr);
+            if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess)
+            {
+                d = nullptr;
+                (void)hipGetLastError();
+            }
+        }
         else
             (void)hipGetLastError();
     }
@@ -77,34 +130,138 @@ struct Pin
     }
 };
 
-struct Set
+// A grow-only device (or pinned host) buffer.
+struct Buf
 {
-    hipStream_t s = nullptr;
-    hipEvent_t done = nullptr;
-    void *d_in = nullptr, *d_vals = nullptr, *d_ws = nullptr, *d_start = nullptr;
-    uint64_t * d_off = nullptr;
-    uint64_t * h_off = nullptr; // pinned, chunk-local offsets
-    size_t in_cap = 0, ws_cap = 0;
-    ~Set()
+    void * p = nullptr;
+    size_t cap = 0;
+    bool host = false;
+    explicit Buf(bool h = false) : host(h) { }
+    void * get(size_t n)
     {
-        if (s)
-            (void)hipStreamSynchronize(s);
-        for (void * p : {d_in, d_vals, d_ws, d_start, static_cast<void *>(d_off)})
-            if (p)
-                (void)hipFree(p);
-        if (h_off)
-            (void)hipHostFree(h_off);
-        if (done)
-            (void)hipEventDestroy(done);
-        if (s)
-            (void)hipStreamDestroy(s);
+        if (n <= cap && p)
+            return p;
+        release();
+        n = std::max<size_t>(n, 256);
+        if (host)
+            hc(hipHostMalloc(&p, n, hipHostMallocDefault), "hipHostMalloc staging");
+        else
+            hc(hipMalloc(&p, n), "hipMalloc staging");
+        cap = n;
+        return p;
+    }
+    void release()
+    {
+        if (p)
+            (void)(host ? hipHostFree(p) : hipFree(p));
+        p = nullptr;
+        cap = 0;
+    }
+    ~Buf() { release(); }
+};
+
+// One pipeline slot: per-chunk buffers; events: `up` = the chunk's uploads
+// landed (copy stream), `mid` = encode offsets reached the host, `done` = the
+// kernel stream finished with the slot.
+struct Slot
+{
+    hipEvent_t up = nullptr, mid = nullptr, done = nullptr;
+    Buf in, vals, ws, start, off, hoff{true};
+    Slot()
+    {
+        for (hipEvent_t * e : {&up, &mid, &done})
+            hc(hipEventCreateWithFlags(e, hipEventDisableTiming), "event");
+    }
+    ~Slot()
+    {
+        for (hipEvent_t e : {up, mid, done})
+            if (e)
+                (void)hipEventDestroy(e);
     }
 };
+
+struct Pipeline
+{
+    int dev = -1;
+    hipStream_t cs = nullptr, ks = nullptr; // copy stream, kernel stream
+    Slot slots[kSlots];
+    explicit Pipeline(int d) : dev(d)
+    {
+        hc(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "stream");
+        hc(hipStreamCreateWithFlags(&ks, hipStreamNonBlocking), "stream");
+    }
+    ~Pipeline()
+    {
+        for (hipStream_t s : {cs, ks})
+            if (s)
+            {
+                (void)hipStreamSynchronize(s);
+                (void)hipStreamDestroy(s);
+            }
+    }
+};
+
+std::mutex g_pool_mu;
+std::vector<Pipeline *> g_pool; // idle pipelines (any device)
+
+// Exclusive use of a pooled pipeline for one call; on return the streams are
+// drained and the pipeline goes back to the pool (or is dropped after an
+// error, when its state is unknown).
+struct Lease
+{
+    Pipeline * p = nullptr;
+    bool ok = false;
+    Lease()
+    {
+        int dev = 0;
+        hc(hipGetDevice(&dev), "hipGetDevice");
+        {
+            std::lock_guard<std::mutex> g(g_pool_mu);
+            for (size_t i = 0; i < g_pool.size(); ++i)
+                if (g_pool[i]->dev == dev)
+                {
+                    p = g_pool[i];
+                    g_pool.erase(g_pool.begin() + static_cast<std::ptrdiff_t>(i));
+                    break;
+                }
+        }
+        if (!p)
+            p = new Pipeline(dev);
+    }
+    ~Lease()
+    {
+        const bool drained = hipStreamSynchronize(p->ks) == hipSuccess && hipStreamSynchronize(p->cs) == hipSuccess;
+        if (ok && drained)
+        {
+            std::lock_guard<std::mutex> g(g_pool_mu);
+            g_pool.push_back(p);
+        }
+        else
+            delete p;
+    }
+};
+
+int report(const std::exception & e, int code)
+{
+    tpf::set_last_error(e.what());
+    return code;
+}
+
+void need_device()
+{
+    int cnt = 0;
+    if (hipGetDeviceCount(&cnt) != hipSuccess || cnt <= 0)
+        throw Err(TPF_ENODEV, "no HIP device visible (turbopfor_amd has no CPU fallback)");
+}
 
 } // namespace
 
 extern "C" {
 
+// Decode: chunk k's bytes (+ offsets, starts) go up by SDMA on the copy
+// stream while the kernel stream decodes chunk k-1 into HBM and downloads it
+// (or, TPF_HOST_DOWN=kernel with a mappable host array, decodes straight
+// into host memory).
 int tpf_host_dec(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_t * h_off, uint64_t nblocks, unsigned n,
                  void * h_vals, const void * h_starts)
 {
@@ -112,9 +269,7 @@ int tpf_host_dec(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_
     {
         if (nblocks == 0)
             return TPF_OK;
-        int cnt = 0;
-        if (hipGetDeviceCount(&cnt) != hipSuccess || cnt <= 0)
-            throw Err(TPF_ENODEV, "no HIP device visible (turbopfor_amd has no CPU fallback)");
+        need_device();
         std::vector<uint64_t> scanned;
         if (!h_off)
         {
@@ -125,65 +280,63 @@ int tpf_host_dec(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_
         }
         const size_t es = wide_fmt(fmt) ? 8 : 4;
         const size_t uv = unit_values(fmt, n);
-        const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(nblocks, (256ull << 20) / (es * uv)));
+        const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(nblocks, chunk_value_bytes() / (es * uv)));
         Pin pin_in(h_in, in_bytes), pin_vals(h_vals, nblocks * uv * es);
-        Set sets[kSets];
+        uint8_t * dv = sdma_down() ? nullptr : static_cast<uint8_t *>(pin_vals.d);
         size_t max_in = 0;
         for (uint64_t c0 = 0; c0 < nblocks; c0 += chunk)
         {
             const uint64_t c1 = std::min(nblocks, c0 + chunk);
             max_in = std::max<size_t>(max_in, h_off[c1] - h_off[c0]);
         }
-        for (Set & st : sets)
-        {
-            hc(hipStreamCreateWithFlags(&st.s, hipStreamNonBlocking), "stream");
-            hc(hipEventCreateWithFlags(&st.done, hipEventDisableTiming), "event");
-            hc(hipMalloc(&st.d_in, max_in + 64), "hipMalloc in");
-            hc(hipMalloc(&st.d_vals, chunk * uv * es), "hipMalloc vals");
-            hc(hipMalloc(reinterpret_cast<void **>(&st.d_off), (chunk + 1) * 8), "hipMalloc off");
-            hc(hipHostMalloc(reinterpret_cast<void **>(&st.h_off), (chunk + 1) * 8, hipHostMallocDefault), "hipHostMalloc off");
-            if (h_starts)
-                hc(hipMalloc(&st.d_start, chunk * es), "hipMalloc starts");
-        }
+        Lease lease;
+        Pipeline & P = *lease.p;
         uint64_t k = 0;
         for (uint64_t c0 = 0; c0 < nblocks; c0 += chunk, ++k)
         {
-            Set & st = sets[k % kSets];
-            hc(hipEventSynchronize(st.done), "wait set"); // h_off staging and buffers free again
+            Slot & sl = P.slots[k % kSlots];
+            hc(hipEventSynchronize(sl.done), "wait slot"); // chunk k-kSlots is done with the slot
             const uint64_t c1 = std::min(nblocks, c0 + chunk);
             const uint64_t nb = c1 - c0;
             const uint64_t b0 = h_off[c0], bytes = h_off[c1] - b0;
+            auto * d_in = static_cast<uint8_t *>(sl.in.get(max_in + 64));
+            auto * d_off = static_cast<uint64_t *>(sl.off.get((chunk + 1) * 8));
+            auto * st_off = static_cast<uint64_t *>(sl.hoff.get((chunk + 1) * 8));
+            void * d_start = h_starts ? sl.start.get(chunk * es) : nullptr;
+            void * out = dv ? static_cast<void *>(dv + c0 * uv * es) : sl.vals.get(chunk * uv * es);
             for (uint64_t i = 0; i <= nb; ++i)
-                st.h_off[i] = h_off[c0 + i] - b0;
-            hc(hipMemcpyAsync(st.d_off, st.h_off, (nb + 1) * 8, hipMemcpyHostToDevice, st.s), "H2D off");
-            hc(hipMemcpyAsync(st.d_in, h_in + b0, bytes, hipMemcpyHostToDevice, st.s), "H2D bytes");
+                st_off[i] = h_off[c0 + i] - b0;
+            hc(hipMemcpyAsync(d_off, st_off, (nb + 1) * 8, hipMemcpyHostToDevice, P.cs), "H2D off");
+            hc(hipMemcpyAsync(d_in, h_in + b0, bytes, hipMemcpyHostToDevice, P.cs), "H2D bytes");
             if (h_starts)
-                hc(hipMemcpyAsync(st.d_start, static_cast<const uint8_t *>(h_starts) + c0 * es, nb * es, hipMemcpyHostToDevice, st.s),
+                hc(hipMemcpyAsync(d_start, static_cast<const uint8_t *>(h_starts) + c0 * es, nb * es, hipMemcpyHostToDevice, P.cs),
                    "H2D starts");
-            const int rc = tpf_dec_batch(fmt, static_cast<const uint8_t *>(st.d_in), bytes, st.d_off, nb, n, st.d_vals,
-                                         h_starts ? st.d_start : nullptr, nullptr, st.s);
-            if (rc != TPF_OK)
-                throw Err(rc, tpf_last_error());
-            hc(hipMemcpyAsync(static_cast<uint8_t *>(h_vals) + c0 * uv * es, st.d_vals, nb * uv * es, hipMemcpyDeviceToHost, st.s),
-               "D2H vals");
-            hc(hipEventRecord(st.done, st.s), "record");
+            hc(hipEventRecord(sl.up, P.cs), "record up");
+            hc(hipStreamWaitEvent(P.ks, sl.up, 0), "wait up");
+            tc(tpf_dec_batch(fmt, d_in, bytes, d_off, nb, n, out, d_start, nullptr, P.ks));
+            if (!dv)
+                hc(hipMemcpyAsync(static_cast<uint8_t *>(h_vals) + c0 * uv * es, out, nb * uv * es, hipMemcpyDeviceToHost, P.ks),
+                   "D2H vals");
+            hc(hipEventRecord(sl.done, P.ks), "record done");
         }
-        for (Set & st : sets)
-            hc(hipStreamSynchronize(st.s), "sync");
+        hc(hipStreamSynchronize(P.ks), "sync");
+        lease.ok = true;
         return TPF_OK;
     }
     catch (const Err & e)
     {
-        tpf::set_last_error(e.what());
-        return e.code;
+        return report(e, e.code);
     }
     catch (const std::exception & e)
     {
-        tpf::set_last_error(e.what());
-        return TPF_EHIP;
+        return report(e, TPF_EHIP);
     }
 }
 
+// Encode: chunk k's values go up by SDMA on the copy stream; the kernel
+// stream encodes it and brings its offsets to the host; once the host knows
+// where chunk k-1 lands (one-chunk lag), the kernel stream downloads chunk
+// k-1's bytes into the host stream, concurrently with the next upload.
 int tpf_host_enc(int fmt, const void * h_vals, uint64_t nblocks, unsigned n, int d1, const void * h_starts, uint64_t start0,
                  uint8_t * h_out, uint64_t out_cap, uint64_t * h_off)
 {
@@ -194,64 +347,58 @@ int tpf_host_enc(int fmt, const void * h_vals, uint64_t nblocks, unsigned n, int
         h_off[0] = 0;
         if (nblocks == 0)
             return TPF_OK;
-        int cnt = 0;
-        if (hipGetDeviceCount(&cnt) != hipSuccess || cnt <= 0)
-            throw Err(TPF_ENODEV, "no HIP device visible (turbopfor_amd has no CPU fallback)");
+        need_device();
         const size_t es = wide_fmt(fmt) ? 8 : 4;
         const size_t uv = unit_values(fmt, n);
-        const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(nblocks, (256ull << 20) / (es * uv)));
+        const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(nblocks, chunk_value_bytes() / (es * uv)));
         Pin pin_vals(h_vals, nblocks * uv * es), pin_out(h_out, out_cap);
-        Set sets[kSets];
+        uint8_t * dout = sdma_down() ? nullptr : static_cast<uint8_t *>(pin_out.d);
         const size_t cap = tpf_enc_bound(fmt, chunk, n);
         const size_t wsb = std::max<size_t>(tpf_enc_workspace_size(fmt, chunk, n), 256);
-        for (Set & st : sets)
-        {
-            hc(hipStreamCreateWithFlags(&st.s, hipStreamNonBlocking), "stream");
-            hc(hipEventCreateWithFlags(&st.done, hipEventDisableTiming), "event");
-            hc(hipMalloc(&st.d_in, cap), "hipMalloc out");
-            hc(hipMalloc(&st.d_vals, chunk * uv * es), "hipMalloc vals");
-            hc(hipMalloc(&st.d_ws, wsb), "hipMalloc ws");
-            hc(hipMalloc(reinterpret_cast<void **>(&st.d_off), (chunk + 1) * 8), "hipMalloc off");
-            hc(hipHostMalloc(reinterpret_cast<void **>(&st.h_off), (chunk + 1) * 8, hipHostMallocDefault), "hipHostMalloc off");
-            if (d1 && h_starts)
-                hc(hipMalloc(&st.d_start, chunk * es), "hipMalloc starts");
-        }
-        // chunk k is encoded on set k%kSets; its bytes are copied out once the
-        // previous chunk's total (its host position) is known: one-chunk lag.
+        Lease lease;
+        Pipeline & P = *lease.p;
         uint64_t pos = 0;
         std::vector<uint64_t> c0s;
         auto finish = [&](uint64_t kk) {
-            Set & st = sets[kk % kSets];
-            hc(hipEventSynchronize(st.done), "wait offsets");
+            Slot & sl = P.slots[kk % kSlots];
+            hc(hipEventSynchronize(sl.mid), "wait offsets");
             const uint64_t c0 = c0s[kk];
             const uint64_t nb = std::min(nblocks, c0 + chunk) - c0;
-            const uint64_t total = st.h_off[nb];
+            const auto * st_off = static_cast<const uint64_t *>(sl.hoff.p);
+            const uint64_t total = st_off[nb];
             if (pos + total > out_cap)
                 throw Err(TPF_EINVAL, "tpf_host_enc: out_cap too small");
             for (uint64_t i = 1; i <= nb; ++i)
-                h_off[c0 + i] = pos + st.h_off[i];
-            hc(hipMemcpyAsync(h_out + pos, st.d_in, total, hipMemcpyDeviceToHost, st.s), "D2H bytes");
-            hc(hipEventRecord(st.done, st.s), "record");
+                h_off[c0 + i] = pos + st_off[i];
+            if (dout)
+                tc(tpf_copy_async(dout + pos, sl.in.p, total, P.ks));
+            else
+                hc(hipMemcpyAsync(h_out + pos, sl.in.p, total, hipMemcpyDeviceToHost, P.ks), "D2H bytes");
+            hc(hipEventRecord(sl.done, P.ks), "record done");
             pos += total;
         };
         uint64_t k = 0;
         for (uint64_t c0 = 0; c0 < nblocks; c0 += chunk, ++k)
         {
-            if (k >= 1)
-                finish(k - 1);
-            Set & st = sets[k % kSets];
-            hc(hipEventSynchronize(st.done), "wait set");
+            Slot & sl = P.slots[k % kSlots];
+            hc(hipEventSynchronize(sl.done), "wait slot");
             c0s.push_back(c0);
             const uint64_t nb = std::min(nblocks, c0 + chunk) - c0;
-            hc(hipMemcpyAsync(st.d_vals, static_cast<const uint8_t *>(h_vals) + c0 * uv * es, nb * uv * es, hipMemcpyHostToDevice, st.s),
+            auto * d_pk = static_cast<uint8_t *>(sl.in.get(cap));
+            void * d_vals = sl.vals.get(chunk * uv * es);
+            void * d_ws = sl.ws.get(wsb);
+            auto * d_off = static_cast<uint64_t *>(sl.off.get((chunk + 1) * 8));
+            void * st_off = sl.hoff.get((chunk + 1) * 8);
+            hc(hipMemcpyAsync(d_vals, static_cast<const uint8_t *>(h_vals) + c0 * uv * es, nb * uv * es, hipMemcpyHostToDevice, P.cs),
                "H2D vals");
             const void * dstart = nullptr;
             uint64_t s0 = start0;
             if (d1 && h_starts)
             {
-                hc(hipMemcpyAsync(st.d_start, static_cast<const uint8_t *>(h_starts) + c0 * es, nb * es, hipMemcpyHostToDevice, st.s),
+                void * d_start = sl.start.get(chunk * es);
+                hc(hipMemcpyAsync(d_start, static_cast<const uint8_t *>(h_starts) + c0 * es, nb * es, hipMemcpyHostToDevice, P.cs),
                    "H2D starts");
-                dstart = st.d_start;
+                dstart = d_start;
             }
             else if (d1 && c0 > 0)
             {
@@ -260,28 +407,38 @@ int tpf_host_enc(int fmt, const void * h_vals, uint64_t nblocks, unsigned n, int
                 s0 = 0;
                 std::memcpy(&s0, last, es);
             }
-            const int rc = tpf_enc_batch(fmt, st.d_vals, nb, n, d1, dstart, s0, static_cast<uint8_t *>(st.d_in), cap, st.d_off,
-                                         st.d_ws, wsb, st.s);
-            if (rc != TPF_OK)
-                throw Err(rc, tpf_last_error());
-            hc(hipMemcpyAsync(st.h_off, st.d_off, (nb + 1) * 8, hipMemcpyDeviceToHost, st.s), "D2H off");
-            hc(hipEventRecord(st.done, st.s), "record");
+            hc(hipEventRecord(sl.up, P.cs), "record up");
+            hc(hipStreamWaitEvent(P.ks, sl.up, 0), "wait up");
+            tc(tpf_enc_batch(fmt, d_vals, nb, n, d1, dstart, s0, d_pk, cap, d_off, d_ws, wsb, P.ks));
+            hc(hipMemcpyAsync(st_off, d_off, (nb + 1) * 8, hipMemcpyDeviceToHost, P.ks), "D2H offsets");
+            hc(hipEventRecord(sl.mid, P.ks), "record offsets");
+            if (k >= 1)
+                finish(k - 1);
         }
         finish(k - 1);
-        for (Set & st : sets)
-            hc(hipStreamSynchronize(st.s), "sync");
+        hc(hipStreamSynchronize(P.ks), "sync");
+        lease.ok = true;
         return TPF_OK;
     }
     catch (const Err & e)
     {
-        tpf::set_last_error(e.what());
-        return e.code;
+        return report(e, e.code);
     }
     catch (const std::exception & e)
     {
-        tpf::set_last_error(e.what());
-        return TPF_EHIP;
+        return report(e, TPF_EHIP);
     }
+}
+
+void tpf_host_release(void)
+{
+    std::vector<Pipeline *> idle;
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        idle.swap(g_pool);
+    }
+    for (Pipeline * p : idle)
+        delete p;
 }
 
 } // extern "C"

@@ -24,6 +24,10 @@ enum : int
     FMT_256V64 = 5,
 };
 
+// Kernel copy (16-B non-temporal stores) for moving data to/from pinned host
+// memory concurrently with an SDMA copy in the other direction (host_copy.hip).
+hipError_t launch_copy(void * dst, const void * src, uint64_t bytes, hipStream_t s);
+
 size_t generic_workspace(uint64_t nblocks);
 hipError_t launch_dec_generic(int fmt, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t n,
                               void * out, const void * starts, unsigned long long * err, hipStream_t s);
