@@ -10,6 +10,9 @@ decode is verified bit-exact at full size afterwards.  One step = one
 tpf_p4dec256v32_batch launch over the whole shard, inputs resident in HBM.
 
 Other workloads (--workload, one JSON line each, for DESIGN.md):
+  c1      BASELINE configs[0]: p4Enc32/p4Dec32, n = 127, bw 8, 0% exceptions --
+          the reference's own CPU case (ab_test single-block loop, cpu_baseline)
+          beside a device batch of 10M such blocks (horizontal format kernels)
   c3      p4D1Dec256v32 on Zipf posting lists (5% big gaps), per-block starts
   c3chain the same list decoded as ONE chained list (only start0 given)
   c4      p4Enc256v32 + p4Dec256v32 round trip (0/5/10/25% exceptions) and
@@ -474,6 +477,68 @@ def run_c4(args, world, rank, dev, T):
                 args.warmup, elapsed, "u32", "synthetic (GPU-generated)", cfg), ok and ok64
 
 
+def cpu_abtest_c1(vals_host, blk_host, blen, n):
+    """ab_test methodology (benchmarks/ab_test.cpp:553-701) on the reference
+    library built from its own sources (oracle/_ref): one L1-hot block,
+    1000 warm-up calls, 10,000-call chunks, best of 3; turbopfor::p4Dec32 /
+    p4Enc32 dispatch path, one core."""
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libtpref.so")
+    if not os.path.exists(ref_so):
+        return None
+    L = ctypes.CDLL(ref_so)
+    f = L.tpref_abtest_p4_32
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint, ctypes.c_int,
+                  ctypes.c_int]
+    f.restype = ctypes.c_double
+    dec_s = f(vals_host.ctypes.data, blk_host.ctypes.data, n, 10000, 3, 1, 0)
+    enc_s = f(vals_host.ctypes.data, blk_host.ctypes.data, n, 10000, 3, 1, 1)
+    try:
+        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:
+        model = "unknown"
+    return {"value": round(n / dec_s / 1e9, 3), "unit": "G int32/s", "cores": 1, "kind": "reference",
+            "sample": f"ab_test loop: one {blen}-B block (n={n}, bw 8, 0% exc), L1-hot, 10,000-call chunks, "
+                      f"best of 3, turbopfor::p4Dec32 (oracle/_ref) on {model}",
+            "dec_MBps_compressed": round(blen / dec_s / 1e6, 1),
+            "enc_G_int32_per_s": round(n / enc_s / 1e9, 3)}
+
+
+def run_c1(args, world, rank, dev, T):
+    """configs[0]: p4Enc32/p4Dec32 with n = 127, bit width 8, no exceptions
+    (values uniform in [0, 255] as ab_test.cpp:1610-1631).  Device: a batch of
+    nblocks such blocks, encoded and decoded by the horizontal-format kernels
+    (tpf_enc_batch / tpf_dec_batch, TPF_FMT_32)."""
+    n = 127
+    nb = args.nblocks
+    g = torch.Generator(device=dev)
+    g.manual_seed(42 + 8 + n + rank)
+    vals = torch.randint(0, 256, (nb * n,), device=dev, generator=g, dtype=torch.int32)
+    packed, offs = tpf.enc_batch("32", vals, nb, n)
+    out = torch.empty_like(vals)
+    elapsed, kern_ms = T.run(lambda: tpf.dec_batch("32", packed, offs, nb, n, out=out), args.steps, args.warmup)
+    ok = bool(torch.equal(out, vals))
+    _, enc_ms = T.run(lambda: tpf.enc_batch("32", vals, nb, n), max(2, args.steps // 4), 1)
+    if rank != 0:
+        return None
+    pbytes = int(packed.numel())
+    value = nb * n * world / (elapsed / args.steps) / 1e9
+    avg_ms = float(np.mean(kern_ms))
+    alg = pbytes + nb * (n * 4 + 8) + 8
+    roof = {"bound": "hbm", "achieved": round(alg / (avg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel_ms_avg": round(avg_ms, 4), "kernel": "tpf::dev::k_dec_g<H32> (horizontal p4Dec32 batch)"}
+    cpu = None
+    if not args.no_cpu_baseline:
+        blen = int(offs[1].item())
+        blk = np.concatenate([packed[:blen].cpu().numpy(), np.zeros(64, np.uint8)])  # + the reference's read slack
+        cpu = cpu_abtest_c1(vals[:n].cpu().numpy().view(np.uint32).copy(), blk, blen, n)
+    cfg = {"workload": "C1: p4Enc32/p4Dec32, n=127, bw 8, 0% exceptions (configs[0]); device batch of n=127 blocks",
+           "nblocks_per_gpu": nb, "bytes_per_block": round(pbytes / nb, 2), "verified": ok,
+           "enc32_G_int32_per_s": round(nb * n / (float(np.mean(enc_ms)) * 1e-3) / 1e9, 2), "parallelism": f"shard{world}"}
+    return line("G int32/s device-resident p4Dec32 (n=127)", value, "G int32/s", world, args.steps, args.warmup,
+                elapsed, "u32", "synthetic (GPU-generated uniform [0,255], GPU-encoded)", cfg, roof, cpu), ok
+
+
 # -------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -482,7 +547,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--nblocks", type=int, default=10_000_000, help="blocks per GPU (shard)")
     ap.add_argument("--exc", type=float, default=10.0)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c3chain", "c4"])
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c3chain", "c4"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sweep", action="store_true", help="c2: also time each bw segment (stderr table)")
     ap.add_argument("--e2e", action="store_true", help="c2: also measure the pinned host-memory path")
@@ -506,7 +571,9 @@ def main():
         else:
             torch.distributed.init_process_group(backend)
     T = Timer(dist_on, dev)
-    if args.workload == "c2":
+    if args.workload == "c1":
+        res = run_c1(args, world, rank, dev, T)
+    elif args.workload == "c2":
         res = run_c2(args, world, rank, dev, T)
     elif args.workload == "c3":
         res = run_c3(args, world, rank, dev, T, chained=False)

@@ -130,4 +130,44 @@ double tpref_abtest_dec256v32(const uint8_t * blk, unsigned iters, unsigned runs
     return best;
 }
 
+// The same methodology for configs[0] of BASELINE.json (C1): p4Enc32 /
+// p4Dec32 of one n-value block (ab_test.cpp:1610-1631 uses n = 127, bw 8).
+// enc != 0 times the encoder on `vals`, else the decoder on `blk`.  Returns
+// best seconds per call.
+double tpref_abtest_p4_32(const uint32_t * vals, const uint8_t * blk, unsigned n, unsigned iters, unsigned runs,
+                          int use_dispatch, int enc)
+{
+    alignas(64) uint32_t in[256 + 64];
+    alignas(64) uint32_t out[256 + 64];
+    alignas(64) uint8_t buf[256 * 5 + 512];
+    std::memcpy(in, vals, n * sizeof(uint32_t));
+    volatile uint32_t sink = 0;
+    auto call = [&](unsigned i) {
+        if (enc)
+        {
+            uint8_t * e = use_dispatch ? turbopfor::p4Enc32(in, n, buf) : turbopfor::scalar::p4Enc32(in, n, buf);
+            sink = sink + static_cast<uint32_t>(e - buf) + buf[i & 63u];
+        }
+        else
+        {
+            use_dispatch ? (void)turbopfor::p4Dec32(blk, n, out) : (void)turbopfor::scalar::p4Dec32(blk, n, out);
+            sink = sink + out[i % n];
+        }
+    };
+    for (unsigned w = 0; w < 1000; ++w)
+        call(w);
+    double best = 1e30;
+    for (unsigned r = 0; r < runs; ++r)
+    {
+        auto t0 = std::chrono::steady_clock::now();
+        for (unsigned i = 0; i < iters; ++i)
+            call(i);
+        auto t1 = std::chrono::steady_clock::now();
+        const double sec = std::chrono::duration<double>(t1 - t0).count() / iters;
+        if (sec < best)
+            best = sec;
+    }
+    return best;
+}
+
 } // extern "C"
