@@ -285,11 +285,18 @@ def run_c2(args, world, rank, dev, T):
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / 10
+            # the segment's data-movement probe (same loads and stores, no decode)
+            e0.record()
+            for _ in range(10):
+                tpf.probe256v32(sub_in, sub_off, hi - lo, sub_out)
+            e1.record()
+            torch.cuda.synchronize()
+            pms = e0.elapsed_time(e1) / 10
             nbytes = int(off_host[hi] - off_host[lo])
             gint = (hi - lo) * 256 / ms / 1e6
             gbs = (nbytes + (hi - lo) * 1032) / ms / 1e6
             log(f"[sweep] bw={s + 1:2d} B/blk={nbytes / (hi - lo):7.1f} ms={ms:.4f} Gint/s={gint:8.1f} "
-                f"alg GB/s={gbs:7.1f} ({gbs / HBM_PEAK_GBS:.1%} of peak)")
+                f"alg GB/s={gbs:7.1f} ({gbs / HBM_PEAK_GBS:.1%} of peak, {pms / ms:.1%} of probe)")
 
     e2e = None
     if args.e2e and rank == 0:
