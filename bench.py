@@ -185,14 +185,38 @@ def cpu_baseline(packed_host, off_host, nblocks, budget_s=12.0, threads=None):
         model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except Exception:
         model = "unknown"
+    abt = abtest_single_block(packed_host, off_host, nblocks) if kind == "reference" else None
     return {
         "value": round(value, 3),
         "unit": "G int32/s",
         "cores": threads,
         "kind": kind,
+        "abtest_single_block": abt,
         "sample": f"{nb} blocks (first 1/16 of each bw segment of the same C2 stream) x {reps} passes, "
                   f"{threads} threads, {what} on {model}",
     }
+
+
+def abtest_single_block(packed_host, off_host, nblocks):
+    """SURVEY §8(d) CPU baseline (i): the ab_test methodology
+    (benchmarks/ab_test.cpp:553-701) -- one block L1-hot, 1000 warm-up calls,
+    10,000-call chunks, best of 3 -- on one core, for the first block of the
+    bw 8, 16 and 24 segments, reference AVX2 dispatch and reference scalar."""
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libtpref.so")
+    L = ctypes.CDLL(ref_so)
+    f = L.tpref_abtest_dec256v32
+    f.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_uint, ctypes.c_int]
+    f.restype = ctypes.c_double
+    res = {}
+    for bw in (8, 16, 24):
+        i = (nblocks * (bw - 1)) // 32
+        b0, b1 = int(off_host[i]), int(off_host[i + 1])
+        blk = np.concatenate([packed_host[b0:b1], np.zeros(64, np.uint8)])  # + the reference's read slack
+        avx2 = f(blk.ctypes.data, 10000, 3, 1)
+        scal = f(blk.ctypes.data, 10000, 3, 0)
+        res[f"bw{bw}"] = {"block_bytes": b1 - b0, "avx2_G_int32_per_s": round(256 / avx2 / 1e9, 3),
+                          "scalar_G_int32_per_s": round(256 / scal / 1e9, 3)}
+    return res
 
 
 # -------------------------------------------------------------- timing core
@@ -313,6 +337,7 @@ def run_c2(args, world, rank, dev, T):
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("c2", nb),
             "kernel": "tpf::dev::k_dec256v32w<StartMode::None>", "kernel_ms_avg": round(avg_ms, 4),
+            "kernel_ms_median": round(float(np.median(kern_ms)), 4), "kernel_ms_min": round(float(np.min(kern_ms)), 4),
             "alg_bytes_per_launch": int(alg),
             "alg_bytes_def": "packed block bytes + 1024 B decoded + 8 B offset per block",
             "probe_GBps": round(probe, 1), "frac_of_probe": round(achieved / probe, 4),
