@@ -11,6 +11,7 @@
 // (src/scalar/p4enc256v64_scalar.cpp:15-30, p4d1dec256v64_scalar.cpp:15-49).
 #include <hipcub/hipcub.hpp>
 
+#include "p4_dec_run.h"
 #include "p4_generic.h"
 #include "tpf_kernels.h"
 
@@ -107,6 +108,88 @@ __global__ __launch_bounds__(256) void k_dec_g(const uint8_t * __restrict in, ui
             atomicMin(err, static_cast<unsigned long long>(blk));
         wave_lds_sync();
     }
+}
+
+// Run-pipelined decode for the one-block units (H32, V128, V256 n != 256,
+// H64): every wave owns a contiguous run of kGRun blocks, the run's
+// control plane lives in vector lanes and the bytes of the next NC-1 blocks
+// are in flight while one decodes (RunPlaneT, p4_dec_run.h -- the machinery
+// of the 256v32 hot path).  k_dec_g above loaded one block, waited, decoded:
+// 0.20 of HBM peak on a batch of p4Dec32 n=127 blocks (bench.py c1).
+constexpr uint32_t kGRun = 16;
+
+template <Fmt F, bool D1, uint32_t NC = 3>
+__global__ __launch_bounds__(256) void k_dec_gr(const uint8_t * __restrict in, uint64_t in_bytes, const uint64_t * __restrict off,
+                                                 uint64_t nblocks, uint32_t n, typename FmtTraits<F>::T * __restrict out,
+                                                 const typename FmtTraits<F>::T * __restrict starts,
+                                                 unsigned long long * __restrict err)
+{
+    using G = UnitGeom<F, false>;
+    using T = typename FmtTraits<F>::T;
+    __shared__ uint32_t slots[4][G::kSlot / 4];
+    __shared__ T scratch[4][512];
+    const uint32_t t = threadIdx.x & 63u;
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    uint32_t * slot = slots[wv];
+    const uint64_t in_base = reinterpret_cast<uint64_t>(in);
+    const uint64_t in_end = in_base + in_bytes;
+    const uint32_t pu = G::per_unit(n);
+    const uint32_t NE = FmtTraits<F>::N ? FmtTraits<F>::N : n;
+    const uint64_t first = (static_cast<uint64_t>(blockIdx.x) * 4u + wv) * kGRun;
+    if (first >= nblocks)
+        return;
+    const uint32_t nr = static_cast<uint32_t>(min_u64(kGRun, nblocks - first));
+    const bool valid = t < nr;
+    const uint64_t o = valid ? off[first + t] : 0ull;
+    const uint64_t e = valid ? off[first + t + 1u] : 0ull;
+    RunPlaneT<G::kSlot> P;
+    P.init(in_base, in_end, o, e, valid);
+    const T startv = (D1 && valid) ? starts[first + t] : T(0);
+    uint64_t badmask = 0u;
+    auto consume = [&](const Chunk & c, uint32_t jj) {
+        const uint32_t ctl = P.stage(c, jj, slot, t);
+        T v[4];
+        uint32_t cm;
+        const uint32_t used = decode_block_g<F>(slot, (ctl >> kCtlShift) & 15u, n, scratch[wv], t, v, &cm);
+        if constexpr (D1)
+        {
+            T st;
+            if constexpr (sizeof(T) == 8)
+                st = readlane_u64(startv, jj);
+            else
+                st = rl(startv, jj);
+            (void)delta1_g<T>(v, n, st, t);
+        }
+        const uint32_t lim = cm ? n : NE;
+        T * op = out + (first + jj) * pu;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+            if (t + 64u * j < lim)
+                op[t + 64u * j] = v[j];
+        wave_lds_sync();
+        if (used != rl(P.len, jj))
+            badmask |= 1ull << jj;
+    };
+    Chunk C[NC];
+#pragma unroll
+    for (uint32_t u = 0; u + 1 < NC; ++u)
+        P.template issue<0>(C[u], u, t);
+    bool more = true;
+    for (uint32_t j = 0; more; j += NC)
+    {
+#pragma unroll
+        for (uint32_t u = 0; u < NC; ++u)
+        {
+            if (more)
+            {
+                P.template issue<0>(C[(u + NC - 1) % NC], j + u + NC - 1, t);
+                consume(C[u], j + u);
+                more = j + u + 1 < nr;
+            }
+        }
+    }
+    if (err != nullptr && t == 0 && badmask != 0u)
+        atomicMin(err, static_cast<unsigned long long>(first + __builtin_ctzll(badmask)));
 }
 
 template <Fmt F, bool D1, bool PAIR>
@@ -250,6 +333,18 @@ hipError_t dec_fmt(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, 
                    const void * starts, unsigned long long * err, hipStream_t s)
 {
     using T = typename dev::FmtTraits<F>::T;
+    if constexpr (!PAIR)
+    {
+        const uint64_t per_wg = 4ull * dev::kGRun;
+        const uint32_t g = static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg);
+        if (starts)
+            hipLaunchKernelGGL((dev::k_dec_gr<F, true>), dim3(g), dim3(256), 0, s, in, in_bytes, off, nblocks, n,
+                               static_cast<T *>(out), static_cast<const T *>(starts), err);
+        else
+            hipLaunchKernelGGL((dev::k_dec_gr<F, false>), dim3(g), dim3(256), 0, s, in, in_bytes, off, nblocks, n,
+                               static_cast<T *>(out), static_cast<const T *>(nullptr), err);
+        return hipGetLastError();
+    }
     const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>((nblocks + 3) / 4, grid_cap(s, 8)));
     if (starts)
         hipLaunchKernelGGL((dev::k_dec_g<F, true, PAIR>), dim3(grid), dim3(256), 0, s, in, in_bytes, off, nblocks, n,
