@@ -165,7 +165,7 @@ __global__ __launch_bounds__(256) void k_dec_gr(const uint8_t * __restrict in, u
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j)
             if (t + 64u * j < lim)
-                op[t + 64u * j] = v[j];
+                __builtin_nontemporal_store(v[j], op + t + 64u * j);
         wave_lds_sync();
         if (used != rl(P.len, jj))
             badmask |= 1ull << jj;
