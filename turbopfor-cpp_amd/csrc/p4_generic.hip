@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void k_dec_g(const uint8_t * __restrict in, ui
 // 0.20 of HBM peak on a batch of p4Dec32 n=127 blocks (bench.py c1).
 constexpr uint32_t kGRun = 16;
 
-template <Fmt F, bool D1, uint32_t NC = 3>
+template <Fmt F, bool D1, uint32_t NC = 4>
 __global__ __launch_bounds__(256) void k_dec_gr(const uint8_t * __restrict in, uint64_t in_bytes, const uint64_t * __restrict off,
                                                  uint64_t nblocks, uint32_t n, typename FmtTraits<F>::T * __restrict out,
                                                  const typename FmtTraits<F>::T * __restrict starts,
