@@ -558,7 +558,7 @@ def run_c1(args, world, rank, dev, T):
     alg = pbytes + nb * (n * 4 + 8) + 8
     roof = {"bound": "hbm", "achieved": round(alg / (avg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel_ms_avg": round(avg_ms, 4), "kernel": "tpf::dev::k_dec_g<H32> (horizontal p4Dec32 batch)"}
+            "kernel_ms_avg": round(avg_ms, 4), "kernel": "tpf::dev::k_dec_gr<H32> (run-pipelined horizontal p4Dec32 batch)"}
     cpu = None
     if not args.no_cpu_baseline:
         blen = int(offs[1].item())
