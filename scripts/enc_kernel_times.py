@@ -1,0 +1,24 @@
+"""Encoder kernel timing (measurement tool; run under rocprofv3 --kernel-trace
+--stats for per-kernel times): C4-mix 256v32 encode, `reps` launches.
+usage: python scripts/enc_kernel_times.py [nblocks] [reps]"""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "turbopfor-cpp_amd", "python"))
+sys.path.insert(0, ROOT)
+import turbopfor_amd as tpf  # noqa: E402
+import bench  # noqa: E402
+
+nb = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+dev = torch.device("cuda:0")
+vals, _ = bench.gen_c2(nb, 0, seed=11, dev=dev, pcts=[0, 5, 10, 25])
+cap = int(tpf.lib().tpf_p4enc256v32_bound(nb))
+out = torch.empty(cap, dtype=torch.uint8, device=dev)
+for _ in range(reps):
+    tpf.enc256v32(vals, out=out)
+torch.cuda.synchronize()
+print("done", os.environ.get("TPF_ENC_PROBE", "0"))

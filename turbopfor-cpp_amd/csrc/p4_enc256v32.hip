@@ -14,7 +14,15 @@
 // Both kernels walk runs of 16 consecutive blocks per wave with the values of
 // the next two blocks in flight (the first version loaded one block per loop
 // iteration and waited for it: 5.0 and 5.4 ms per 10M blocks, latency-bound).
+//
+// TPF_ENC_PROBE (measurement only -- the output is NOT a valid stream): 1 =
+// plan kernel with the cost model replaced by a wave OR, 2 = write kernel
+// copying the staged values instead of building blocks; same loads and
+// stores, so they time each pass's data-movement ceiling
+// (scripts/gpu_enc_probe.sh, profiles/r1_v4_enc_probe.txt).
 #include <hipcub/hipcub.hpp>
+
+#include <cstdlib>
 
 #include "p4_enc32.h"
 #include "tpf_kernels.h"
@@ -119,7 +127,7 @@ __device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t lane)
     return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(lane)));
 }
 
-template <bool D1>
+template <bool D1, int PROBE = 0>
 __global__ __launch_bounds__(256) void k_enc256v32_plan(const uint32_t * __restrict in, uint64_t nblocks,
                                                          const uint32_t * __restrict starts, uint32_t start0,
                                                          uint64_t * __restrict sizes, uint32_t * __restrict plan)
@@ -137,7 +145,17 @@ __global__ __launch_bounds__(256) void k_enc256v32_plan(const uint32_t * __restr
     R.walk(t, [&](u32x4 v, uint32_t jj) {
         if constexpr (D1)
             v = delta_encode(v, rl32(stv, jj), t);
-        const Plan32 P = plan_block256(v, hist[wv], t);
+        Plan32 P;
+        if constexpr (PROBE == 1)
+        {
+            P.b = bw32(uni(wave_or(v.x | v.y | v.z | v.w)));
+            P.bx = 0;
+            P.size = 1 + 32 * P.b;
+            P.xn = 0;
+            P.raw = 0;
+        }
+        else
+            P = plan_block256(v, hist[wv], t);
         szv = t == jj ? P.size : szv;
         pwv = t == jj ? plan_word(P) : pwv;
     });
@@ -148,7 +166,7 @@ __global__ __launch_bounds__(256) void k_enc256v32_plan(const uint32_t * __restr
     }
 }
 
-template <bool D1>
+template <bool D1, int PROBE = 0>
 __global__ __launch_bounds__(256) void k_enc256v32_write(const uint32_t * __restrict in, uint64_t nblocks,
                                                           const uint32_t * __restrict starts, uint32_t start0,
                                                           const uint64_t * __restrict off, const uint32_t * __restrict plan,
@@ -179,6 +197,14 @@ __global__ __launch_bounds__(256) void k_enc256v32_write(const uint32_t * __rest
         const uint32_t size = rl32(szv, jj);
         const Plan32 P = unplan(rl32(pwv, jj), size);
         const uint64_t dst = out_base + ((static_cast<uint64_t>(rl32(ohi, jj)) << 32) | rl32(olo, jj));
+        if constexpr (PROBE == 2)
+        {
+            reinterpret_cast<u32x4 *>(img)[4 + t] = v;
+            wave_lds_sync();
+            copy_out_image16(img, kImgLead, dst, size, cap_end, t);
+            wave_lds_sync();
+            return;
+        }
         const uint32_t sb = emit_block256(img, val_all[wv], P, v, t);
         wave_lds_sync();
         copy_out_image16(img, sb, dst, size, cap_end, t);
@@ -215,8 +241,12 @@ hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_
     size_t scan_bytes = ws_bytes > plan_bytes ? ws_bytes - plan_bytes : 0;
     const uint64_t per_wg = 4ull * dev::kEncRun;
     const uint32_t grid = static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg);
+    const char * pe = std::getenv("TPF_ENC_PROBE");
+    const int probe = pe ? std::atoi(pe) : 0;
     if (d1)
         hipLaunchKernelGGL(dev::k_enc256v32_plan<true>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan);
+    else if (probe == 1)
+        hipLaunchKernelGGL((dev::k_enc256v32_plan<false, 1>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan);
     else
         hipLaunchKernelGGL(dev::k_enc256v32_plan<false>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan);
     hipError_t e = hipGetLastError();
@@ -227,6 +257,9 @@ hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_
         return e;
     if (d1)
         hipLaunchKernelGGL(dev::k_enc256v32_write<true>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
+                           out, out_cap);
+    else if (probe == 2)
+        hipLaunchKernelGGL((dev::k_enc256v32_write<false, 2>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
                            out, out_cap);
     else
         hipLaunchKernelGGL(dev::k_enc256v32_write<false>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
