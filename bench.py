@@ -123,6 +123,7 @@ def pmc_traffic(workload, nblocks):
         d = json.load(open(PROFILE_TRAFFIC))
     except Exception:
         return None
+    d = d.get(workload, {}) if "workload" not in d else d
     if d.get("workload") != workload or int(d.get("nblocks", -1)) != nblocks:
         return None
     return d.get("hbm_bytes_per_launch")
@@ -440,7 +441,8 @@ def run_c3(args, world, rank, dev, T, chained):
     avg_ms = float(np.mean(kern_ms))
     alg = pbytes + nb * (1024 + 8 + (0 if chained else 4)) + 8
     roof = {"bound": "hbm", "achieved": round(alg / (avg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic": None if chained else pmc_traffic("c3", nb),
             "kernel_ms_avg": round(avg_ms, 4),
             "kernel": ("k_dec256v32w<SumOnly> + hipcub scan + k_dec256v32w<Prefix>" if chained
                        else "tpf::dev::k_dec256v32w<StartMode::PerBlock>")}
@@ -557,7 +559,7 @@ def run_c1(args, world, rank, dev, T):
     avg_ms = float(np.mean(kern_ms))
     alg = pbytes + nb * (n * 4 + 8) + 8
     roof = {"bound": "hbm", "achieved": round(alg / (avg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("c1", nb),
             "kernel_ms_avg": round(avg_ms, 4), "kernel": "tpf::dev::k_dec_gr<H32> (run-pipelined horizontal p4Dec32 batch)"}
     cpu = None
     if not args.no_cpu_baseline:

@@ -16,5 +16,5 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_stats -
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $R/gpurun_out/bench_pmcf.json 2>&1 || { echo "pmc fetch rc=$?"; tail -20 $R/gpurun_out/bench_pmcf.json; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $R/gpurun_out/bench_pmcw.json 2>&1 || { echo "pmc write rc=$?"; tail -20 $R/gpurun_out/bench_pmcw.json; exit 1; }
 cd $R
-python3 scripts/pmc_traffic.py gpurun_out/pmc_fetch/run_counter_collection.csv gpurun_out/pmc_write/run_counter_collection.csv 10000000 gpurun_out/pmc_traffic.json
+python3 scripts/pmc_traffic.py c2 gpurun_out/pmc_fetch/run_counter_collection.csv gpurun_out/pmc_write/run_counter_collection.csv 10000000 gpurun_out/pmc_traffic.json
 find gpurun_out/prof_stats -name "*.csv" | head
