@@ -320,6 +320,210 @@ __global__ __launch_bounds__(256) void k_enc_g(const typename FmtTraits<F>::T * 
             off[nblocks] = 0;
 }
 
+// ---- run-pipelined encode for the one-block units ------------------------
+// Same plan -> scan -> write scheme as k_enc_g, but every wave owns a
+// contiguous run of kGRun units whose values arrive through one buffer
+// descriptor with the next NC-1 units in flight (k_enc_g loaded a unit, waited
+// and planned: latency-bound, 169 G int32/s on p4Enc32 n=127 batches).
+template <Fmt F>
+struct EncRunG
+{
+    using T = typename FmtTraits<F>::T;
+    uint64_t first;
+    uint32_t nr, pu, NE;
+    __amdgpu_buffer_rsrc_t rs;
+
+    __device__ __forceinline__ bool init(const T * in, uint64_t nblocks, uint32_t wv, uint32_t n)
+    {
+        first = (static_cast<uint64_t>(blockIdx.x) * 4u + wv) * kGRun;
+        if (first >= nblocks)
+            return false;
+        nr = static_cast<uint32_t>(min_u64(kGRun, nblocks - first));
+        pu = UnitGeom<F, false>::per_unit(n);
+        NE = FmtTraits<F>::N ? FmtTraits<F>::N : n;
+        rs = make_rsrc(in + first * pu, nr * pu * static_cast<uint32_t>(sizeof(T)));
+        return true;
+    }
+
+    // unit jj's elements t + 64j (zero past NE or past the run: out-of-range offsets)
+    __device__ __forceinline__ void load(uint32_t jj, uint32_t t, T v[4]) const
+    {
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+        {
+            const uint32_t e = t + 64u * j;
+            const uint32_t o = (e < NE && jj < nr) ? (jj * pu + e) * static_cast<uint32_t>(sizeof(T)) : 0x80000000u;
+            if constexpr (sizeof(T) == 8)
+            {
+                const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, static_cast<int>(o), 0, 0);
+                v[j] = (static_cast<uint64_t>(x[1]) << 32) | x[0];
+            }
+            else
+                v[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(o), 0, 0);
+        }
+    }
+
+    // delta-1 start of unit first+t (lanes t < nr): the given starts, or for
+    // one chained list the last value of the previous unit
+    __device__ __forceinline__ T start_lane(const T * in, const T * starts, T start0, uint32_t t) const
+    {
+        if (t >= nr)
+            return T(0);
+        const uint64_t blk = first + t;
+        if (starts)
+            return starts[blk];
+        return blk == 0 ? start0 : in[blk * pu - 1u];
+    }
+};
+
+// deltaEnc1 (p4_scalar_internal.h:711-719) over elements e < n in order.
+template <class T>
+__device__ __forceinline__ void delta_enc_g(T v[4], T prev0, uint32_t n, uint32_t t)
+{
+    T d[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j)
+    {
+        T prev;
+        if constexpr (sizeof(T) == 8)
+        {
+            const uint32_t lo = static_cast<uint32_t>(__shfl_up(static_cast<int>(static_cast<uint32_t>(v[j])), 1, 64));
+            const uint32_t hi = static_cast<uint32_t>(__shfl_up(static_cast<int>(static_cast<uint32_t>(v[j] >> 32)), 1, 64));
+            prev = (static_cast<uint64_t>(hi) << 32) | lo;
+            if (t == 0)
+                prev = j == 0 ? prev0 : readlane64(v[j - 1], 63);
+        }
+        else
+        {
+            prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(v[j]), 1, 64));
+            if (t == 0)
+                prev = j == 0 ? prev0 : __builtin_amdgcn_readlane(v[j - 1], 63);
+        }
+        d[j] = (t + 64u * j < n) ? T(v[j] - prev - 1u) : T(0);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j)
+        v[j] = d[j];
+}
+
+template <class T>
+struct Unit4
+{
+    T v[4];
+};
+
+template <Fmt F, bool D1, bool WRITE, uint32_t NC = 3>
+__global__ __launch_bounds__(256) void k_enc_gr(const typename FmtTraits<F>::T * __restrict in, uint64_t nblocks, uint32_t n,
+                                                 const typename FmtTraits<F>::T * __restrict starts,
+                                                 typename FmtTraits<F>::T start0, uint64_t * __restrict off,
+                                                 uint8_t * __restrict out, uint64_t out_cap)
+{
+    using G = UnitGeom<F, false>;
+    using T = typename FmtTraits<F>::T;
+    __shared__ uint32_t imgs[WRITE ? 4 : 1][WRITE ? (G::kSlot / 4 + 8) : 1];
+    __shared__ __attribute__((aligned(16))) uint32_t hist[4][kPlanGHistU32];
+    const uint32_t t = threadIdx.x & 63u;
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    if constexpr (!WRITE)
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            off[nblocks] = 0; // exclusive scan over nblocks+1 entries yields the total
+    EncRunG<F> R;
+    if (!R.init(in, nblocks, wv, n))
+        return;
+    const T stv = D1 ? R.start_lane(in, starts, start0, t) : T(0);
+    uint32_t szv = 0u;
+    uint32_t olo = 0u, ohi = 0u;
+    if constexpr (WRITE)
+    {
+        const uint64_t ov = t < R.nr ? off[R.first + t] : 0ull;
+        const uint64_t ev = t < R.nr ? off[R.first + t + 1u] : 0ull;
+        szv = static_cast<uint32_t>(ev - ov);
+        olo = static_cast<uint32_t>(ov);
+        ohi = static_cast<uint32_t>(ov >> 32);
+    }
+    const uint64_t out_base = reinterpret_cast<uint64_t>(out);
+    const uint64_t cap_end = out_base + out_cap;
+    uint32_t * img = imgs[wv];
+    auto body = [&](Unit4<T> & U, uint32_t jj) {
+        if constexpr (D1)
+        {
+            T st;
+            if constexpr (sizeof(T) == 8)
+                st = readlane_u64(stv, jj);
+            else
+                st = static_cast<T>(__builtin_amdgcn_readlane(static_cast<int>(stv), static_cast<int>(jj)));
+            delta_enc_g<T>(U.v, st, n, t);
+        }
+        const PlanG P = plan_block_g<F>(U.v, n, hist[wv], t);
+        if constexpr (!WRITE)
+        {
+            szv = t == jj ? P.size : szv;
+        }
+        else
+        {
+            const uint32_t size = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(szv), static_cast<int>(jj)));
+            const uint64_t o = (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ohi), static_cast<int>(jj)))) << 32)
+                             | static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(olo), static_cast<int>(jj)));
+            const uint64_t dst = out_base + o;
+            const uint32_t phase = static_cast<uint32_t>(dst & 3u);
+            emit_block_g<F>(img, phase, P, U.v, n, t);
+            wave_lds_sync();
+            const uint64_t a0 = dst & ~3ull;
+            const uint32_t end = phase + size;
+            const uint32_t nd = (end + 3u) >> 2;
+            for (uint32_t d = t; d < nd; d += 64u)
+            {
+                const uint64_t ga = a0 + 4u * d;
+                const uint32_t w = img[d];
+                const uint32_t lo = 4u * d, hi = lo + 4u;
+                if (lo >= phase && hi <= end && ga + 4u <= cap_end)
+                    *reinterpret_cast<uint32_t *>(ga) = w;
+                else
+                    for (uint32_t x = 0; x < 4; ++x)
+                    {
+                        const uint32_t bi = lo + x;
+                        if (bi >= phase && bi < end && ga + x < cap_end)
+                            *reinterpret_cast<uint8_t *>(ga + x) = static_cast<uint8_t>(w >> (8u * x));
+                    }
+            }
+            wave_lds_sync();
+            // only dwords [0, nd) can be non-zero: clear them for the next unit
+            for (uint32_t d = t; d < nd; d += 64u)
+                img[d] = 0u;
+            wave_lds_sync();
+        }
+    };
+    if constexpr (WRITE)
+    {
+        for (uint32_t i = t; i < G::kSlot / 4 + 8; i += 64u)
+            img[i] = 0u;
+        wave_lds_sync();
+    }
+    // NC units rotate in registers (loop unrolled by NC, no copies of
+    // in-flight loads): while unit j is encoded, j+1 .. j+NC-1 are in flight.
+    Unit4<T> C[NC];
+#pragma unroll
+    for (uint32_t u = 0; u + 1 < NC; ++u)
+        R.load(u, t, C[u].v);
+    bool more = true;
+    for (uint32_t j = 0; more; j += NC)
+    {
+#pragma unroll
+        for (uint32_t u = 0; u < NC; ++u)
+        {
+            if (more)
+            {
+                R.load(j + u + NC - 1, t, C[(u + NC - 1) % NC].v);
+                body(C[u], j + u);
+                more = j + u + 1 < R.nr;
+            }
+        }
+    }
+    if constexpr (!WRITE)
+        if (t < R.nr)
+            off[R.first + t] = szv;
+}
+
 } // namespace tpf::dev
 
 namespace tpf
@@ -360,9 +564,26 @@ hipError_t enc_fmt_d(const void * in, uint64_t nblocks, uint32_t n, const void *
                      uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t s)
 {
     using T = typename dev::FmtTraits<F>::T;
-    const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>((nblocks + 3) / 4, grid_cap(s, 8)));
     const T * ip = static_cast<const T *>(in);
     const T * sp = static_cast<const T *>(starts);
+    if constexpr (!PAIR)
+    {
+        const uint64_t per_wg = 4ull * dev::kGRun;
+        const uint32_t g = static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg);
+        hipLaunchKernelGGL((dev::k_enc_gr<F, D1, false>), dim3(g), dim3(256), 0, s, ip, nblocks, n, sp, static_cast<T>(start0), off,
+                           out, out_cap);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess)
+            return e;
+        size_t sb = ws_bytes;
+        e = hipcub::DeviceScan::ExclusiveSum(ws, sb, off, static_cast<int>(nblocks + 1), s);
+        if (e != hipSuccess)
+            return e;
+        hipLaunchKernelGGL((dev::k_enc_gr<F, D1, true>), dim3(g), dim3(256), 0, s, ip, nblocks, n, sp, static_cast<T>(start0), off,
+                           out, out_cap);
+        return hipGetLastError();
+    }
+    const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>((nblocks + 3) / 4, grid_cap(s, 8)));
     hipLaunchKernelGGL((dev::k_enc_g<F, D1, PAIR, false>), dim3(grid), dim3(256), 0, s, ip, nblocks, n, sp,
                        static_cast<T>(start0), off, out, out_cap);
     hipError_t e = hipGetLastError();
