@@ -110,3 +110,24 @@ def test_p4enc32_vs_oracle(n):
     np.testing.assert_array_equal(packed.cpu().numpy(), exp_packed)
     out = tpf.dec_batch("32", packed, offs, nb, n)
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32).reshape(nb, n), vals)
+
+
+@pytest.mark.parametrize("n", [127, 256])
+def test_p4dec32_corrupt_offsets_reported(n):
+    """The run-pipelined generic decoder reports the first block whose parsed
+    length disagrees with the offsets (d_err), like the 256v32 kernel."""
+    rng = np.random.default_rng(7 + n)
+    nb = 300
+    vals = rng.integers(0, 1 << 11, size=(nb, n), dtype=np.uint64).astype(np.uint32)
+    exp_packed, exp_off = oracle_lib.enc32_batch(vals)
+    packed = torch.from_numpy(exp_packed).to(DEV)
+    bad = exp_off.astype(np.int64).copy()
+    bad[200] += 1  # block 199 looks one byte longer, block 200 one shorter
+    err = torch.zeros(1, dtype=torch.int64, device=DEV)
+    tpf.dec_batch("32", packed, torch.from_numpy(bad).to(DEV), nb, n, err=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 199
+    out = tpf.dec_batch("32", packed, torch.from_numpy(exp_off.astype(np.int64)).to(DEV), nb, n, err=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == -1  # UINT64_MAX: every block consistent
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32).reshape(nb, n), vals)
