@@ -437,17 +437,23 @@ def run_c3(args, world, rank, dev, T, chained):
         fn = lambda: tpf.dec256v32(packed, offs, nb, out=out, starts=starts)
     elapsed, kern_ms = T.run(fn, args.steps, args.warmup)
     ok = bool(torch.equal(out, vals)) if (not chained or world == 1) else True
+    # data-movement probe of the same stream (decode kernel's loads and stores, no decode)
+    _, probe_ms = T.run(lambda: tpf.probe256v32(packed, offs, nb, out), 10, 2)
     if rank != 0:
         return None
     value = nb * 256 * world / (elapsed / args.steps) / 1e9
     avg_ms = float(np.mean(kern_ms))
     alg = pbytes + nb * (1024 + 8 + (0 if chained else 4)) + 8
+    probe_alg = pbytes + nb * (1024 + 8) + 8
     roof = {"bound": "hbm", "achieved": round(alg / (avg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "traffic": None if chained else pmc_traffic("c3", nb),
             "kernel_ms_avg": round(avg_ms, 4),
             "kernel": ("k_dec256v32w<SumOnly> + hipcub scan + k_dec256v32w<Prefix>" if chained
-                       else "tpf::dev::k_dec256v32w<StartMode::PerBlock>")}
+                       else "tpf::dev::k_dec256v32w<StartMode::PerBlock>"),
+            "probe_GBps": round(probe_alg / (float(np.mean(probe_ms)) * 1e-3) / 1e9, 1),
+            "ms_vs_probe": round(avg_ms / float(np.mean(probe_ms)), 3),
+            "probe_def": "tpf_probe256v32 on the same stream (loads + stores, no decode; no starts read)"}
     cfg = {"workload": "C3: p4D1Dec256v32 " + ("chained list (start0 only)" if chained else "per-block starts")
                        + ", Zipf(1.1) gaps on [1,64] + 5% 64+U[0,2^16)",
            "nblocks_per_gpu": nb, "bytes_per_int": round(pbytes / nb / 256, 4), "vbyte_block_frac": round(vb_frac, 4),
