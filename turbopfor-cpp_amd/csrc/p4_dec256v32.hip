@@ -48,8 +48,9 @@ struct DecArgs
 // copied (a copy forces s_waitcnt vmcnt(0)).  No workgroup barriers at all.
 // The run's control plane lives in vector lanes (RunPlane, p4_dec_run.h).
 // Measured and kept: runs of 16 (8: same, 32..62: -2..-5%),
-// three chunks at 7 waves/SIMD (four at 6: same).
-template <StartMode SM, uint32_t kRun, uint32_t POL = 2, uint32_t NC = 3, int MINW = 7>
+// three chunks at 7 waves/SIMD (four at 6: same); with ONE (the default
+// launch), chunks are one 16-byte load each and six are in flight.
+template <StartMode SM, uint32_t kRun, uint32_t POL = 2, uint32_t NC = 3, int MINW = 7, bool ONE = false>
 __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
 {
     __shared__ uint32_t slots[4][kSlotBytes / 4];
@@ -75,7 +76,7 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
     const uint64_t blk = first + stride * t;
     const uint64_t o = valid ? A.off[blk] : 0ull;
     const uint64_t e = valid ? A.off[blk + 1u] : 0ull;
-    RunPlane P;
+    RunPlaneT<kSlotBytes, ONE> P;
     P.init(in_base, in_end, o, e, valid);
     uint32_t startv = 0u;
     if constexpr (SM == StartMode::PerBlock)
@@ -87,11 +88,12 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
     uint64_t badmask = 0u;
     constexpr bool sum_pass = SM == StartMode::SumOnly;
 
-    auto issue = [&](Chunk & c, uint32_t jj) { P.issue<POL>(c, jj, t); };
+    auto issue = [&](Chunk & c, uint32_t jj) { P.template issue<POL>(c, jj, t); };
     auto consume = [&](const Chunk & c, uint32_t jj) {
         if constexpr (SM == StartMode::Probe)
         {
-            st16<POL>(reinterpret_cast<u32x4 *>(out_run + jj * stride * 256u) + t, c.a | c.b);
+            st16<POL>(reinterpret_cast<u32x4 *>(out_run + jj * stride * 256u) + t,
+                      ONE ? (c.a | P.big_rest_or(jj, t)) : (c.a | c.b));
             return;
         }
         const uint32_t ctl = P.stage(c, jj, slot, t);
@@ -167,12 +169,26 @@ uint32_t dec_pol()
     return v;
 }
 
+// Layout of the loads in flight (A/B knob TPF_DEC_ONE, default 1): ONE =
+// one 16-byte load per lane per block (its first 1 KB; a bigger block's rest
+// is loaded when it is staged) with six blocks in flight, instead of two
+// loads per block (2 KB window) with three.  Same registers; measured on one
+// box, alternating: C2 899 -> 906, C3 1080 -> 1106 G int32/s, probes +0..4%.
+bool one_layout()
+{
+    static const uint32_t knob = env_knob("TPF_DEC_ONE", 1u);
+    return knob != 0u;
+}
+
 template <dev::StartMode SM, uint32_t POL>
 hipError_t launch_pol(const dev::DecArgs & A, hipStream_t stream)
 {
     constexpr uint64_t per_wg = 4ull * dev::kRunDefault;
     const uint32_t grid = static_cast<uint32_t>((A.nblocks + per_wg - 1) / per_wg);
-    hipLaunchKernelGGL((dev::k_dec256v32w<SM, dev::kRunDefault, POL>), dim3(grid), dim3(256), 0, stream, A);
+    if (one_layout())
+        hipLaunchKernelGGL((dev::k_dec256v32w<SM, dev::kRunDefault, POL, 6, 7, true>), dim3(grid), dim3(256), 0, stream, A);
+    else
+        hipLaunchKernelGGL((dev::k_dec256v32w<SM, dev::kRunDefault, POL>), dim3(grid), dim3(256), 0, stream, A);
     return hipGetLastError();
 }
 

@@ -16,6 +16,7 @@ constexpr uint32_t kCtlSpan = 0xFFFu;    // bytes the fast path stages (0: none)
 constexpr uint32_t kCtlShift = 12;       // [12,16): block start inside its 16-aligned chunk
 constexpr uint32_t kCtlSlow = 1u << 16;  // > 2 KB or straddles the stream end: guarded loads
 constexpr uint32_t kCtlTwo = 1u << 17;   // second 1 KB half present
+constexpr uint32_t kCtlBig = 1u << 18;   // ONE layout: bytes past the first 1 KB, loaded at staging
 
 struct Chunk
 {
@@ -50,7 +51,10 @@ __device__ __forceinline__ void st16(u32x4 * p, const u32x4 & v)
 // computed once in VALU and fetched per block with v_readlane.  The scalar
 // unit is shared by the CU's four SIMDs; per-block 64-bit address arithmetic
 // on it was the measured limiter before this layout.
-template <uint32_t SLOT>
+// ONE: one 16-byte load per lane per block in flight (the block's first
+// 1 KB; the rest of a larger block is loaded when it is staged), so twice as
+// many blocks fit in flight in the same registers.
+template <uint32_t SLOT, bool ONE = false>
 struct RunPlaneT
 {
     uint32_t ctl;        // kCtl* bits
@@ -65,9 +69,9 @@ struct RunPlaneT
         const uint64_t cb = ab & ~15ull;
         span = valid ? static_cast<uint32_t>(min_u64(sub_sat(in_base + e, cb), SLOT - 64)) : 0u;
         avail = valid ? static_cast<uint32_t>(min_u64(sub_sat(in_end, cb), SLOT)) : 0u;
-        const bool slow = valid && (span > 2048u || span + 16u > avail);
+        const bool slow = valid && ((!ONE && span > 2048u) || span + 16u > avail);
         ctl = (slow ? 0u : span) | ((static_cast<uint32_t>(ab) & 15u) << kCtlShift) | (slow ? kCtlSlow : 0u)
-            | (!slow && span > 1024u ? kCtlTwo : 0u);
+            | (!ONE && !slow && span > 1024u ? kCtlTwo : 0u) | (ONE && !slow && span > 1024u ? kCtlBig : 0u);
         len = (e >= o && e - o < 0x10000ull) ? static_cast<uint32_t>(e - o) : 0xFFFFFFFFu;
         cblo = static_cast<uint32_t>(cb);
         cbhi = static_cast<uint32_t>(cb >> 32);
@@ -84,7 +88,8 @@ struct RunPlaneT
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(base), SLOT);
         const uint32_t fspan = cw & kCtlSpan;
         c.a = ld16<POL>(rs, 16u * t < fspan ? 16u * t : 0x80000000u);
-        c.b = ld16<POL>(rs, 1024u + 16u * t < fspan ? 1024u + 16u * t : 0x80000000u);
+        if constexpr (!ONE)
+            c.b = ld16<POL>(rs, 1024u + 16u * t < fspan ? 1024u + 16u * t : 0x80000000u);
     }
 
     // First 4 bytes of block jj (wave-uniform), from the load registers:
@@ -102,13 +107,38 @@ struct RunPlaneT
         return uni(__builtin_amdgcn_alignbyte(hi, lo, s & 3u));
     }
 
+    // Probe mode (no staging): the same extra loads of a big block, OR-ed.
+    __device__ __forceinline__ u32x4 big_rest_or(uint32_t jj, uint32_t t) const
+    {
+        u32x4 acc{0u, 0u, 0u, 0u};
+        const uint32_t cw = rl(ctl, jj);
+        if (ONE && (cw & kCtlBig))
+        {
+            const uint32_t sp = cw & kCtlSpan;
+            const uint64_t base = (static_cast<uint64_t>(rl(cbhi, jj)) << 32) | rl(cblo, jj);
+            const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(base), SLOT);
+            for (uint32_t x = 1024u + 16u * t; x < sp; x += 1024u)
+                acc |= ld16<0>(rs, x);
+        }
+        return acc;
+    }
+
     // Write block jj's chunk into the wave's LDS slot; returns its ctl word.
     __device__ __forceinline__ uint32_t stage(const Chunk & c, uint32_t jj, uint32_t * slot, uint32_t t) const
     {
         const uint32_t cw = rl(ctl, jj);
         reinterpret_cast<u32x4 *>(slot)[t] = c.a;
-        if (cw & kCtlTwo)
+        if (!ONE && (cw & kCtlTwo))
             reinterpret_cast<u32x4 *>(slot)[64 + t] = c.b;
+        if (ONE && (cw & kCtlBig))
+        {
+            // the rest of a block larger than 1 KB (inside the stream: plain loads)
+            const uint32_t sp = cw & kCtlSpan;
+            const uint64_t base = (static_cast<uint64_t>(rl(cbhi, jj)) << 32) | rl(cblo, jj);
+            const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(base), SLOT);
+            for (uint32_t x = 1024u + 16u * t; x < sp; x += 1024u)
+                reinterpret_cast<u32x4 *>(slot)[x >> 4] = ld16<0>(rs, x);
+        }
         if (cw & kCtlSlow)
         {
             // rare: > 2 KB units or the chunk straddling the end of the stream
