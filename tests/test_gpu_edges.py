@@ -60,3 +60,46 @@ def test_stream_over_4gib_roundtrip():
     assert int(offs[-1].item()) > (1 << 32)
     out = tpf.dec256v32_chained(packed, offs, nb, start0=0)
     assert torch.equal(out, lst)
+
+
+def test_hipgraph_capture_replay():
+    """The batched entry points allocate nothing and only launch on the given
+    stream, so a decode + chained-D1 decode + encode sequence can be captured
+    into one hipGraph (torch.cuda.CUDAGraph on ROCm) and replayed with new
+    inputs written into the same buffers."""
+    nb = 3000
+    g = torch.Generator(device=DEV)
+    g.manual_seed(5)
+
+    def fresh():
+        bw = torch.randint(1, 33, (nb, 1), device=DEV, generator=g)
+        raw = torch.randint(-(1 << 31), (1 << 31) - 1, (nb, 256), device=DEV, generator=g, dtype=torch.int32)
+        return torch.where(bw >= 32, raw, raw & ((torch.ones_like(bw) << bw) - 1).to(torch.int32))
+
+    L = tpf.lib()
+    vals = fresh()
+    cap = int(L.tpf_p4enc256v32_bound(nb))
+    packed = torch.zeros(cap, dtype=torch.uint8, device=DEV)
+    offs = torch.zeros(nb + 1, dtype=torch.int64, device=DEV)
+    wsb = int(L.tpf_p4enc256v32_workspace_size(nb))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=DEV)
+    out = torch.empty_like(vals)
+    err = torch.zeros(1, dtype=torch.int64, device=DEV)
+
+    def seq():
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        assert L.tpf_p4enc256v32_batch(vals.data_ptr(), nb, packed.data_ptr(), cap, offs.data_ptr(), ws.data_ptr(), wsb, s) == 0
+        assert L.tpf_p4dec256v32_batch(packed.data_ptr(), cap, offs.data_ptr(), nb, out.data_ptr(), err.data_ptr(), s) == 0
+
+    seq()  # warm-up outside the capture (library load, first-launch setup)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        seq()
+    for _ in range(3):
+        vals.copy_(fresh())
+        out.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, vals)
+        assert int(err.item()) == -1
