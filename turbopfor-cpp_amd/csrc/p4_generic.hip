@@ -1,14 +1,13 @@
 // p4_generic.hip -- batch kernels for the non-hot formats of include/turbopfor.h
-// (32/64-bit horizontal, 128v32, 256v32 with n != 256, 128v64, 256v64) on gfx950.
+// (32/64-bit horizontal, 128v32, 256v32 with n != 256) on gfx950; the
+// 128v64/256v64 units are routed to p4_dec256v64.hip / p4_enc256v64.hip.
 //
-// One block per wave (grid-stride over waves).  Decode stages the block's
-// bytes into a per-wave LDS slot with 16-byte buffer loads and runs
-// decode_block_g (p4_generic.h); encode is the same three-pass scheme as the
-// 256v32 encoder: size pass -> exclusive scan -> write pass (LDS image copied
-// out with dword stores and byte stores on the two shared edge dwords).
-// A "unit" is one reference call: one block, or for 256v64 the pair of
-// 128v64 blocks that p4Enc256v64/p4Dec256v64 emit/consume
-// (src/scalar/p4enc256v64_scalar.cpp:15-30, p4d1dec256v64_scalar.cpp:15-49).
+// Every wave owns a contiguous run of 16 blocks with the next blocks' bytes
+// (or values) in flight.  Decode stages each block into a per-wave LDS slot
+// (RunPlaneT, p4_dec_run.h) and runs decode_block_g (p4_generic.h); encode
+// is the same three-pass scheme as the 256v32 encoder: plan pass -> exclusive
+// scan -> write pass (LDS image copied out with dword stores and byte stores
+// on the two shared edge dwords).
 #include <hipcub/hipcub.hpp>
 
 #include "p4_dec_run.h"
@@ -30,92 +29,13 @@ struct UnitGeom
     }
 };
 
-template <Fmt F, bool D1, bool PAIR>
-__global__ __launch_bounds__(256) void k_dec_g(const uint8_t * __restrict in, uint64_t in_bytes, const uint64_t * __restrict off,
-                                                uint64_t nblocks, uint32_t n, typename FmtTraits<F>::T * __restrict out,
-                                                const typename FmtTraits<F>::T * __restrict starts,
-                                                unsigned long long * __restrict err)
-{
-    using G = UnitGeom<F, PAIR>;
-    using T = typename FmtTraits<F>::T;
-    __shared__ uint32_t slots[4][G::kSlot / 4];
-    __shared__ T scratch[4][512];
-    const uint32_t t = threadIdx.x & 63u;
-    const uint32_t wv = uni(threadIdx.x >> 6);
-    uint32_t * slot = slots[wv];
-    const uint64_t W = static_cast<uint64_t>(gridDim.x) * 4u;
-    const uint64_t in_base = reinterpret_cast<uint64_t>(in);
-    const uint64_t in_end = in_base + in_bytes;
-    const uint32_t ns = G::nsub(n);
-    const uint32_t pu = G::per_unit(n);
-    const uint32_t NE = FmtTraits<F>::N ? FmtTraits<F>::N : ns;
-    // One block in flight: the next block's bytes are loaded into registers
-    // while this one decodes (the first version loaded, waited and decoded
-    // in turn: 0.2 of HBM peak on p4Dec32 n=127 batches).
-    constexpr uint32_t kPre = (G::kSlot + 1023u) / 1024u;
-    uint64_t blk = static_cast<uint64_t>(blockIdx.x) * 4u + wv;
-    if (blk >= nblocks)
-        return;
-    u32x4 R[kPre];
-    uint64_t po = 0, pe = 0, pbase = 0;
-    uint32_t pspan = 0;
-    auto issue = [&](uint64_t b) {
-        po = off[b];
-        pe = off[b + 1];
-        pbase = (in_base + po) & ~15ull;
-        pspan = static_cast<uint32_t>(min_u64(sub_sat(in_base + pe, pbase), G::kSlot - 64));
-        const uint32_t avail = static_cast<uint32_t>(min_u64(sub_sat(in_end, pbase), G::kSlot));
-        const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(pbase), avail);
-#pragma unroll
-        for (uint32_t q = 0; q < kPre; ++q)
-        {
-            const uint32_t x = 16u * t + 1024u * q;
-            R[q] = x < pspan ? load16_guarded(reinterpret_cast<const uint8_t *>(pbase), rs, x, avail) : u32x4{0u, 0u, 0u, 0u};
-        }
-    };
-    issue(blk);
-    for (; blk < nblocks; blk += W)
-    {
-#pragma unroll
-        for (uint32_t q = 0; q < kPre; ++q)
-        {
-            const uint32_t x = 16u * t + 1024u * q;
-            if (x < pspan)
-                reinterpret_cast<u32x4 *>(slot)[x >> 4] = R[q];
-        }
-        wave_lds_sync();
-        const uint64_t o = po, e = pe, base = pbase;
-        if (blk + W < nblocks)
-            issue(blk + W);
-        uint32_t s = static_cast<uint32_t>(in_base + o - base);
-        const uint32_t s0 = s;
-        T start = D1 ? starts[blk] : T(0);
-        for (uint32_t u = 0; u < (PAIR ? 2u : 1u); ++u)
-        {
-            T v[4];
-            uint32_t cm;
-            s += decode_block_g<F>(slot, s, ns, scratch[wv], t, v, &cm);
-            if constexpr (D1)
-                start = delta1_g<T>(v, ns, start, t);
-            const uint32_t lim = cm ? ns : NE;
-            T * op = out + blk * pu + u * 128u;
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j)
-                if (t + 64u * j < lim)
-                    op[t + 64u * j] = v[j];
-        }
-        if (err != nullptr && t == 0 && static_cast<uint64_t>(s - s0) != e - o)
-            atomicMin(err, static_cast<unsigned long long>(blk));
-        wave_lds_sync();
-    }
-}
-
 // Run-pipelined decode for the one-block units (H32, V128, V256 n != 256,
 // H64): every wave owns a contiguous run of kGRun blocks, the run's
 // control plane lives in vector lanes and the bytes of the next NC-1 blocks
 // are in flight while one decodes (RunPlaneT, p4_dec_run.h -- the machinery
-// of the 256v32 hot path).  k_dec_g above loaded one block, waited, decoded:
-// 0.20 of HBM peak on a batch of p4Dec32 n=127 blocks (bench.py c1).
+// of the 256v32 hot path).  The first version (one block per wave, grid
+// stride: load, wait, decode) ran at 0.20 of HBM peak on p4Dec32 n=127
+// batches (bench.py c1); 128v64/256v64 units use p4_dec256v64.hip.
 constexpr uint32_t kGRun = 16;
 
 template <Fmt F, bool D1, uint32_t NC = 4>
@@ -192,139 +112,11 @@ __global__ __launch_bounds__(256) void k_dec_gr(const uint8_t * __restrict in, u
         atomicMin(err, static_cast<unsigned long long>(first + __builtin_ctzll(badmask)));
 }
 
-template <Fmt F, bool D1, bool PAIR>
-__device__ __forceinline__ void load_unit(const typename FmtTraits<F>::T * in, uint64_t blk, uint32_t u, uint32_t n,
-                                          const typename FmtTraits<F>::T * starts, typename FmtTraits<F>::T start0,
-                                          uint32_t t, typename FmtTraits<F>::T v[4])
-{
-    using G = UnitGeom<F, PAIR>;
-    using T = typename FmtTraits<F>::T;
-    const uint32_t pu = G::per_unit(n);
-    const uint32_t ns = G::nsub(n);
-    const uint32_t NE = FmtTraits<F>::N ? FmtTraits<F>::N : ns;
-    const T * ip = in + blk * pu + u * 128u;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j)
-        v[j] = (t + 64u * j < NE) ? ip[t + 64u * j] : T(0);
-    if constexpr (D1)
-    {
-        // deltaEnc1 (p4_scalar_internal.h:711-719): d[e] = x[e] - x[e-1] - 1
-        T prev0;
-        if (u == 1u)
-            prev0 = in[blk * pu + 127u];
-        else if (starts)
-            prev0 = starts[blk];
-        else
-            prev0 = blk == 0 ? start0 : in[blk * pu - 1u]; // chained list
-        T d[4];
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j)
-        {
-            T prev;
-            if constexpr (sizeof(T) == 8)
-            {
-                const uint32_t lo = static_cast<uint32_t>(__shfl_up(static_cast<int>(static_cast<uint32_t>(v[j])), 1, 64));
-                const uint32_t hi = static_cast<uint32_t>(__shfl_up(static_cast<int>(static_cast<uint32_t>(v[j] >> 32)), 1, 64));
-                prev = (static_cast<uint64_t>(hi) << 32) | lo;
-                if (t == 0)
-                    prev = j == 0 ? prev0 : readlane64(v[j - 1], 63);
-            }
-            else
-            {
-                prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(v[j]), 1, 64));
-                if (t == 0)
-                    prev = j == 0 ? prev0 : __builtin_amdgcn_readlane(v[j - 1], 63);
-            }
-            d[j] = (t + 64u * j < ns) ? T(v[j] - prev - 1u) : T(0);
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j)
-            v[j] = d[j];
-    }
-}
-
-// WRITE=false: sizes[blk] = encoded bytes of the unit.  WRITE=true: emit at off[blk].
-template <Fmt F, bool D1, bool PAIR, bool WRITE>
-__global__ __launch_bounds__(256) void k_enc_g(const typename FmtTraits<F>::T * __restrict in, uint64_t nblocks, uint32_t n,
-                                                const typename FmtTraits<F>::T * __restrict starts,
-                                                typename FmtTraits<F>::T start0, uint64_t * __restrict off,
-                                                uint8_t * __restrict out, uint64_t out_cap)
-{
-    using G = UnitGeom<F, PAIR>;
-    using T = typename FmtTraits<F>::T;
-    __shared__ uint32_t imgs[WRITE ? 4 : 1][WRITE ? (G::kSlot / 4 + 8) : 1];
-    __shared__ __attribute__((aligned(16))) uint32_t hist[4][kPlanGHistU32];
-    const uint32_t t = threadIdx.x & 63u;
-    const uint32_t wv = uni(threadIdx.x >> 6);
-    const uint64_t W = static_cast<uint64_t>(gridDim.x) * 4u;
-    const uint32_t ns = G::nsub(n);
-    const uint64_t out_base = reinterpret_cast<uint64_t>(out);
-    for (uint64_t blk = static_cast<uint64_t>(blockIdx.x) * 4u + wv; blk < nblocks; blk += W)
-    {
-        if constexpr (!WRITE)
-        {
-            uint32_t total = 0;
-            for (uint32_t u = 0; u < (PAIR ? 2u : 1u); ++u)
-            {
-                T v[4];
-                load_unit<F, D1, PAIR>(in, blk, u, n, starts, start0, t, v);
-                total += plan_block_g<F>(v, ns, hist[wv], t).size;
-            }
-            if (t == 0)
-                off[blk] = total;
-        }
-        else
-        {
-            uint32_t * img = imgs[wv];
-            for (uint32_t i = t; i < G::kSlot / 4 + 8; i += 64u)
-                img[i] = 0u;
-            wave_lds_sync();
-            const uint64_t o = off[blk];
-            const uint32_t size = static_cast<uint32_t>(off[blk + 1] - o);
-            const uint64_t dst = out_base + o;
-            const uint32_t phase = static_cast<uint32_t>(dst & 3u);
-            uint32_t s = phase;
-            for (uint32_t u = 0; u < (PAIR ? 2u : 1u); ++u)
-            {
-                T v[4];
-                load_unit<F, D1, PAIR>(in, blk, u, n, starts, start0, t, v);
-                const PlanG P = plan_block_g<F>(v, ns, hist[wv], t);
-                emit_block_g<F>(img, s, P, v, ns, t);
-                s += P.size;
-            }
-            wave_lds_sync();
-            const uint64_t a0 = dst & ~3ull;
-            const uint32_t end = phase + size;
-            const uint32_t nd = (end + 3u) >> 2;
-            const uint64_t cap_end = out_base + out_cap;
-            for (uint32_t d = t; d < nd; d += 64u)
-            {
-                const uint64_t ga = a0 + 4u * d;
-                const uint32_t w = img[d];
-                const uint32_t lo = 4u * d, hi = lo + 4u;
-                if (lo >= phase && hi <= end && ga + 4u <= cap_end)
-                    *reinterpret_cast<uint32_t *>(ga) = w;
-                else
-                    for (uint32_t x = 0; x < 4; ++x)
-                    {
-                        const uint32_t bi = lo + x;
-                        if (bi >= phase && bi < end && ga + x < cap_end)
-                            *reinterpret_cast<uint8_t *>(ga + x) = static_cast<uint8_t>(w >> (8u * x));
-                    }
-            }
-            wave_lds_sync();
-        }
-    }
-    if constexpr (!WRITE)
-        if (blockIdx.x == 0 && threadIdx.x == 0)
-            off[nblocks] = 0;
-}
-
 // ---- run-pipelined encode for the one-block units ------------------------
-// Same plan -> scan -> write scheme as k_enc_g, but every wave owns a
+// Plan -> scan -> write as the 256v32 encoder; every wave owns a
 // contiguous run of kGRun units whose values arrive through one buffer
-// descriptor with the next NC-1 units in flight (k_enc_g loaded a unit, waited
-// and planned: latency-bound, 169 G int32/s on p4Enc32 n=127 batches).
+// descriptor with the next NC-1 units in flight (the first version, one unit
+// per wave: latency-bound, 169 G int32/s on p4Enc32 n=127 batches).
 template <Fmt F>
 struct EncRunG
 {
@@ -532,60 +324,33 @@ namespace tpf
 namespace
 {
 
-template <dev::Fmt F, bool PAIR>
+template <dev::Fmt F>
 hipError_t dec_fmt(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t n, void * out,
                    const void * starts, unsigned long long * err, hipStream_t s)
 {
     using T = typename dev::FmtTraits<F>::T;
-    if constexpr (!PAIR)
-    {
-        const uint64_t per_wg = 4ull * dev::kGRun;
-        const uint32_t g = static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg);
-        if (starts)
-            hipLaunchKernelGGL((dev::k_dec_gr<F, true>), dim3(g), dim3(256), 0, s, in, in_bytes, off, nblocks, n,
-                               static_cast<T *>(out), static_cast<const T *>(starts), err);
-        else
-            hipLaunchKernelGGL((dev::k_dec_gr<F, false>), dim3(g), dim3(256), 0, s, in, in_bytes, off, nblocks, n,
-                               static_cast<T *>(out), static_cast<const T *>(nullptr), err);
-        return hipGetLastError();
-    }
-    const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>((nblocks + 3) / 4, grid_cap(s, 8)));
+    const uint64_t per_wg = 4ull * dev::kGRun;
+    const uint32_t g = static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg);
     if (starts)
-        hipLaunchKernelGGL((dev::k_dec_g<F, true, PAIR>), dim3(grid), dim3(256), 0, s, in, in_bytes, off, nblocks, n,
-                           static_cast<T *>(out), static_cast<const T *>(starts), err);
+        hipLaunchKernelGGL((dev::k_dec_gr<F, true>), dim3(g), dim3(256), 0, s, in, in_bytes, off, nblocks, n, static_cast<T *>(out),
+                           static_cast<const T *>(starts), err);
     else
-        hipLaunchKernelGGL((dev::k_dec_g<F, false, PAIR>), dim3(grid), dim3(256), 0, s, in, in_bytes, off, nblocks, n,
-                           static_cast<T *>(out), static_cast<const T *>(nullptr), err);
+        hipLaunchKernelGGL((dev::k_dec_gr<F, false>), dim3(g), dim3(256), 0, s, in, in_bytes, off, nblocks, n, static_cast<T *>(out),
+                           static_cast<const T *>(nullptr), err);
     return hipGetLastError();
 }
 
-template <dev::Fmt F, bool PAIR, bool D1>
+template <dev::Fmt F, bool D1>
 hipError_t enc_fmt_d(const void * in, uint64_t nblocks, uint32_t n, const void * starts, uint64_t start0, uint8_t * out,
                      uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t s)
 {
     using T = typename dev::FmtTraits<F>::T;
     const T * ip = static_cast<const T *>(in);
     const T * sp = static_cast<const T *>(starts);
-    if constexpr (!PAIR)
-    {
-        const uint64_t per_wg = 4ull * dev::kGRun;
-        const uint32_t g = static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg);
-        hipLaunchKernelGGL((dev::k_enc_gr<F, D1, false>), dim3(g), dim3(256), 0, s, ip, nblocks, n, sp, static_cast<T>(start0), off,
-                           out, out_cap);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess)
-            return e;
-        size_t sb = ws_bytes;
-        e = hipcub::DeviceScan::ExclusiveSum(ws, sb, off, static_cast<int>(nblocks + 1), s);
-        if (e != hipSuccess)
-            return e;
-        hipLaunchKernelGGL((dev::k_enc_gr<F, D1, true>), dim3(g), dim3(256), 0, s, ip, nblocks, n, sp, static_cast<T>(start0), off,
-                           out, out_cap);
-        return hipGetLastError();
-    }
-    const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>((nblocks + 3) / 4, grid_cap(s, 8)));
-    hipLaunchKernelGGL((dev::k_enc_g<F, D1, PAIR, false>), dim3(grid), dim3(256), 0, s, ip, nblocks, n, sp,
-                       static_cast<T>(start0), off, out, out_cap);
+    const uint64_t per_wg = 4ull * dev::kGRun;
+    const uint32_t g = static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg);
+    hipLaunchKernelGGL((dev::k_enc_gr<F, D1, false>), dim3(g), dim3(256), 0, s, ip, nblocks, n, sp, static_cast<T>(start0), off, out,
+                       out_cap);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return e;
@@ -593,17 +358,17 @@ hipError_t enc_fmt_d(const void * in, uint64_t nblocks, uint32_t n, const void *
     e = hipcub::DeviceScan::ExclusiveSum(ws, sb, off, static_cast<int>(nblocks + 1), s);
     if (e != hipSuccess)
         return e;
-    hipLaunchKernelGGL((dev::k_enc_g<F, D1, PAIR, true>), dim3(grid), dim3(256), 0, s, ip, nblocks, n, sp,
-                       static_cast<T>(start0), off, out, out_cap);
+    hipLaunchKernelGGL((dev::k_enc_gr<F, D1, true>), dim3(g), dim3(256), 0, s, ip, nblocks, n, sp, static_cast<T>(start0), off, out,
+                       out_cap);
     return hipGetLastError();
 }
 
-template <dev::Fmt F, bool PAIR>
+template <dev::Fmt F>
 hipError_t enc_fmt(const void * in, uint64_t nblocks, uint32_t n, bool d1, const void * starts, uint64_t start0, uint8_t * out,
                    uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t s)
 {
-    return d1 ? enc_fmt_d<F, PAIR, true>(in, nblocks, n, starts, start0, out, out_cap, off, ws, ws_bytes, s)
-              : enc_fmt_d<F, PAIR, false>(in, nblocks, n, starts, start0, out, out_cap, off, ws, ws_bytes, s);
+    return d1 ? enc_fmt_d<F, true>(in, nblocks, n, starts, start0, out, out_cap, off, ws, ws_bytes, s)
+              : enc_fmt_d<F, false>(in, nblocks, n, starts, start0, out, out_cap, off, ws, ws_bytes, s);
 }
 
 } // namespace
@@ -624,14 +389,14 @@ hipError_t launch_dec_generic(int fmt, const uint8_t * in, uint64_t in_bytes, co
     switch (fmt)
     {
         case FMT_32:
-            return dec_fmt<dev::Fmt::H32, false>(in, in_bytes, off, nblocks, n, out, starts, err, s);
+            return dec_fmt<dev::Fmt::H32>(in, in_bytes, off, nblocks, n, out, starts, err, s);
         case FMT_128V32:
-            return dec_fmt<dev::Fmt::V128, false>(in, in_bytes, off, nblocks, n, out, starts, err, s);
+            return dec_fmt<dev::Fmt::V128>(in, in_bytes, off, nblocks, n, out, starts, err, s);
         case FMT_256V32:
-            return dec_fmt<dev::Fmt::V256, false>(in, in_bytes, off, nblocks, n, out, starts, err, s);
+            return dec_fmt<dev::Fmt::V256>(in, in_bytes, off, nblocks, n, out, starts, err, s);
         case FMT_64:
-            return dec_fmt<dev::Fmt::H64, false>(in, in_bytes, off, nblocks, n, out, starts, err, s);
-        case FMT_128V64: // run-pipelined kernel, p4_dec256v64.hip (generic one-block-per-wave: 263 vs 468 G int64/s)
+            return dec_fmt<dev::Fmt::H64>(in, in_bytes, off, nblocks, n, out, starts, err, s);
+        case FMT_128V64: // run-pipelined kernel, p4_dec256v64.hip
             return launch_dec128v64(1, in, in_bytes, off, nblocks, static_cast<uint64_t *>(out),
                                     static_cast<const uint64_t *>(starts), err, s);
         case FMT_256V64:
@@ -652,17 +417,17 @@ hipError_t launch_enc_generic(int fmt, const void * in, uint64_t nblocks, uint32
     switch (fmt)
     {
         case FMT_32:
-            return enc_fmt<dev::Fmt::H32, false>(in, nblocks, n, d1, starts, start0, out, out_cap, off, ws, ws_bytes, s);
+            return enc_fmt<dev::Fmt::H32>(in, nblocks, n, d1, starts, start0, out, out_cap, off, ws, ws_bytes, s);
         case FMT_128V32:
-            return enc_fmt<dev::Fmt::V128, false>(in, nblocks, n, d1, starts, start0, out, out_cap, off, ws, ws_bytes, s);
+            return enc_fmt<dev::Fmt::V128>(in, nblocks, n, d1, starts, start0, out, out_cap, off, ws, ws_bytes, s);
         case FMT_256V32:
-            return enc_fmt<dev::Fmt::V256, false>(in, nblocks, n, d1, starts, start0, out, out_cap, off, ws, ws_bytes, s);
+            return enc_fmt<dev::Fmt::V256>(in, nblocks, n, d1, starts, start0, out, out_cap, off, ws, ws_bytes, s);
         case FMT_64:
-            return enc_fmt<dev::Fmt::H64, false>(in, nblocks, n, d1, starts, start0, out, out_cap, off, ws, ws_bytes, s);
-        case FMT_128V64:
-            return enc_fmt<dev::Fmt::V128X64, false>(in, nblocks, n, d1, starts, start0, out, out_cap, off, ws, ws_bytes, s);
+            return enc_fmt<dev::Fmt::H64>(in, nblocks, n, d1, starts, start0, out, out_cap, off, ws, ws_bytes, s);
+        case FMT_128V64: // run-pipelined kernels, p4_enc256v64.hip
         case FMT_256V64:
-            return enc_fmt<dev::Fmt::V128X64, true>(in, nblocks, n, d1, starts, start0, out, out_cap, off, ws, ws_bytes, s);
+            return launch_enc128v64(fmt == FMT_256V64 ? 2u : 1u, static_cast<const uint64_t *>(in), nblocks, d1,
+                                    static_cast<const uint64_t *>(starts), start0, out, out_cap, off, ws, ws_bytes, s);
         default:
             return hipErrorInvalidValue;
     }
