@@ -69,3 +69,61 @@ def test_roundtrip_large_mixed():
     torch.cuda.synchronize()
     assert int(err.item()) == -1
     assert torch.equal(out, vals.view(nb, 256))
+
+
+def test_full_size_c2_sample_vs_oracle():
+    """At the bench's full size (10M blocks, C2 generator: bw 1..32 segments,
+    10% exceptions) the GPU encoder's bytes for 4,000 sampled blocks equal the
+    oracle's encoding of those blocks, their offsets step by exactly that
+    size, and the GPU decoder returns the sampled blocks' values."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    nb = 10_000_000
+    vals, _ = bench.gen_c2(nb, 10.0, seed=1, dev=torch.device(DEV))
+    packed, offs = tpf.enc256v32(vals)
+    rng = np.random.default_rng(0)
+    idx = np.sort(rng.choice(nb, 4000, replace=False))
+    idx_t = torch.from_numpy(idx).to(DEV)
+    sample = vals[idx_t].cpu().numpy().view(np.uint32)
+    exp_packed, exp_off = oracle_lib.enc256v32_batch(sample)
+    o = offs.cpu().numpy()
+    pk = packed.cpu().numpy()
+    for i, b in enumerate(idx):
+        got = pk[o[b]:o[b + 1]]
+        want = exp_packed[exp_off[i]:exp_off[i + 1]]
+        assert np.array_equal(got, want), f"block {b}"
+    out = tpf.dec256v32(packed, offs, nb)
+    assert torch.equal(out[idx_t], vals[idx_t])
+
+
+def test_full_size_c3_sample_vs_oracle():
+    """Full-size C3 (10M blocks of Zipf posting lists, per-block starts):
+    p4D1Enc256v32 bytes of 4,000 sampled blocks equal the oracle's, and the
+    D1 decode (per-block starts) and the chained decode return them."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    nb = 10_000_000
+    vals, starts = bench.gen_c3(nb, seed=7, dev=torch.device(DEV))
+    packed, offs = tpf.enc256v32(vals, d1=True, starts=starts)
+    rng = np.random.default_rng(1)
+    idx = np.sort(rng.choice(nb, 4000, replace=False))
+    idx_t = torch.from_numpy(idx).to(DEV)
+    sample = vals[idx_t].cpu().numpy().view(np.uint32)
+    sst = starts[idx_t].cpu().numpy().view(np.uint32)
+    exp_packed, exp_off = oracle_lib.enc256v32_batch(sample, starts=sst)
+    o = offs.cpu().numpy()
+    pk = packed.cpu().numpy()
+    for i, b in enumerate(idx):
+        assert np.array_equal(pk[o[b]:o[b + 1]], exp_packed[exp_off[i]:exp_off[i + 1]]), f"block {b}"
+    out = tpf.dec256v32(packed, offs, nb, starts=starts)
+    assert torch.equal(out[idx_t], vals[idx_t])
+    out2 = tpf.dec256v32_chained(packed, offs, nb, start0=int(starts[0].item()) & 0xFFFFFFFF)
+    assert torch.equal(out2, vals)
