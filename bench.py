@@ -187,12 +187,23 @@ def cpu_baseline(packed_host, off_host, nblocks, budget_s=12.0, threads=None):
     except Exception:
         model = "unknown"
     abt = abtest_single_block(packed_host, off_host, nblocks) if kind == "reference" else None
+    scalar = None
+    if kind == "reference":
+        # the reference's scalar path (the parity oracle) over the same sample, shorter budget
+        fs = L.tpref_dec256v32_stream_mt
+        fs(sample.ctypes.data_as(u8p), soff.ctypes.data_as(u64p), nb, out.ctypes.data_as(u32p), threads, 0, 0)
+        stot, sreps, s0 = 0.0, 0, time.perf_counter()
+        while time.perf_counter() - s0 < budget_s / 3:
+            stot += fs(sample.ctypes.data_as(u8p), soff.ctypes.data_as(u64p), nb, out.ctypes.data_as(u32p), threads, 0, 0)
+            sreps += 1
+        scalar = round(nb * 256 * sreps / stot / 1e9, 3)
     return {
         "value": round(value, 3),
         "unit": "G int32/s",
         "cores": threads,
         "kind": kind,
         "abtest_single_block": abt,
+        "scalar_value": scalar,
         "sample": f"{nb} blocks (first 1/16 of each bw segment of the same C2 stream) x {reps} passes, "
                   f"{threads} threads, {what} on {model}",
     }
