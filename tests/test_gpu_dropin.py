@@ -175,3 +175,46 @@ def test_copy_async_phases():
             want = src_h.numpy()
             np.testing.assert_array_equal(got[dp:dp + ln], want[sp:sp + ln], err_msg=f"{sp} {dp} {ln}")
             assert (got[:dp] == 0xAB).all() and (got[dp + ln:dp + ln + 64] == 0xAB).all(), (sp, dp, ln)
+
+
+def test_host_streams_concurrent_threads(monkeypatch):
+    """Two host threads decoding and encoding through the pooled pipelines at
+    once (each call leases its own pipeline; ctypes releases the GIL)."""
+    import threading
+
+    monkeypatch.setenv("TPF_HOST_CHUNK_BYTES", str(300 * 1024))
+    L = capi()
+    L.tpf_host_dec.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                               ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]
+    L.tpf_host_enc.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_int,
+                               ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    jobs = []
+    for seed in (11, 12, 13, 14):
+        blocks = np.concatenate([datagen.c2_blocks(800, bw, 10, seed=seed) for bw in (4, 13, 22, 31)])
+        exp_packed, exp_off = oracle_lib.enc256v32_batch(blocks)
+        jobs.append((blocks, exp_packed, exp_off))
+    errors = []
+
+    def work(blocks, exp_packed, exp_off):
+        try:
+            for _ in range(3):
+                nb = len(blocks)
+                back = np.zeros_like(blocks)
+                assert L.tpf_host_dec(2, exp_packed.ctypes.data, len(exp_packed), exp_off.ctypes.data, nb, 256,
+                                      back.ctypes.data, None) == 0
+                np.testing.assert_array_equal(back, blocks)
+                out = np.zeros(nb * 1100 + 64, dtype=np.uint8)
+                off = np.zeros(nb + 1, dtype=np.uint64)
+                assert L.tpf_host_enc(2, blocks.ctypes.data, nb, 256, 0, None, 0, out.ctypes.data, len(out),
+                                      off.ctypes.data) == 0
+                np.testing.assert_array_equal(off, exp_off)
+                np.testing.assert_array_equal(out[: off[-1]], exp_packed)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    threads = [threading.Thread(target=work, args=j) for j in jobs]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    assert not errors, errors
