@@ -340,6 +340,21 @@ def run_c2(args, world, rank, dev, T):
     # data-movement ceiling of the same access pattern (same kernel, loads
     # and stores only, no decode) -- outside the timed region
     _, probe_ms = T.run(lambda: tpf.probe256v32(packed, offs, nb, out), 10, 2)
+    # STREAM-copy ceiling of this box (SURVEY §8 d): device-to-device copy of
+    # the 10 GB value array into a second buffer (read + write bytes / time)
+    # (rank 0 only, outside T.run: no collective)
+    copy_GBps = None
+    if rank == 0:
+        dst = torch.empty_like(out)
+        dst.copy_(out)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            dst.copy_(out)
+        e1.record()
+        torch.cuda.synchronize()
+        copy_GBps = round(2 * out.numel() * 4 * 5 / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+        del dst
     if rank != 0:
         return None
     avg_ms = float(np.mean(kern_ms))
@@ -353,7 +368,8 @@ def run_c2(args, world, rank, dev, T):
             "alg_bytes_per_launch": int(alg),
             "alg_bytes_def": "packed block bytes + 1024 B decoded + 8 B offset per block",
             "probe_GBps": round(probe, 1), "frac_of_probe": round(achieved / probe, 4),
-            "probe_def": "tpf_probe256v32: the decode kernel's own loads and stores with decoding removed"}
+            "probe_def": "tpf_probe256v32: the decode kernel's own loads and stores with decoding removed",
+            "stream_copy_GBps": copy_GBps}
     # the CPU baseline is timed at N=1 only (a reported baseline, not a per-rank cost)
     cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(packed.cpu().numpy(),
                                                                           offs.cpu().numpy().astype(np.uint64), nb)
