@@ -384,7 +384,12 @@ __device__ __forceinline__ void copy_out_image16(const uint32_t * img, uint32_t 
     const uint8_t * ib = reinterpret_cast<const uint8_t *>(img);
     const uint32_t ph = static_cast<uint32_t>(dst & 15u);
     const uint32_t base = sb - ph;
-    uint8_t * const a16 = reinterpret_cast<uint8_t *>(dst & ~15ull);
+    // global address space: a pointer made from an integer is generic, and
+    // flat stores also count against lgkmcnt, so every later LDS wait of
+    // the wave would wait for these stores to reach memory
+    typedef __attribute__((address_space(1))) uint8_t gu8;
+    typedef __attribute__((address_space(1))) u32x4 gu32x4;
+    gu8 * const a16 = (gu8 *)(dst & ~15ull);
     const uint32_t end = ph + size;
     if (dst + size <= cap_end)
     {
@@ -396,7 +401,7 @@ __device__ __forceinline__ void copy_out_image16(const uint32_t * img, uint32_t 
         {
             const uint32_t q = (base >> 2) + 4u * k;
             const uint32_t w0 = img[q], w1 = img[q + 1], w2 = img[q + 2], w3 = img[q + 3], w4 = img[q + 4];
-            *reinterpret_cast<u32x4 *>(a16 + 16u * k) =
+            *(gu32x4 *)(a16 + 16u * k) =
                 u32x4{__builtin_amdgcn_alignbyte(w1, w0, bs), __builtin_amdgcn_alignbyte(w2, w1, bs),
                       __builtin_amdgcn_alignbyte(w3, w2, bs), __builtin_amdgcn_alignbyte(w4, w3, bs)};
         }

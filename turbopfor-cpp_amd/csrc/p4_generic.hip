@@ -263,19 +263,23 @@ __global__ __launch_bounds__(256) void k_enc_gr(const typename FmtTraits<F>::T *
             const uint64_t a0 = dst & ~3ull;
             const uint32_t end = phase + size;
             const uint32_t nd = (end + 3u) >> 2;
+            // global address space (a pointer made from an integer is generic:
+            // flat stores would also hold up the wave's LDS waits)
+            typedef __attribute__((address_space(1))) uint32_t gu32;
+            typedef __attribute__((address_space(1))) uint8_t gu8;
             for (uint32_t d = t; d < nd; d += 64u)
             {
                 const uint64_t ga = a0 + 4u * d;
                 const uint32_t w = img[d];
                 const uint32_t lo = 4u * d, hi = lo + 4u;
                 if (lo >= phase && hi <= end && ga + 4u <= cap_end)
-                    *reinterpret_cast<uint32_t *>(ga) = w;
+                    *(gu32 *)ga = w;
                 else
                     for (uint32_t x = 0; x < 4; ++x)
                     {
                         const uint32_t bi = lo + x;
                         if (bi >= phase && bi < end && ga + x < cap_end)
-                            *reinterpret_cast<uint8_t *>(ga + x) = static_cast<uint8_t>(w >> (8u * x));
+                            *(gu8 *)(ga + x) = static_cast<uint8_t>(w >> (8u * x));
                     }
             }
             wave_lds_sync();
