@@ -42,14 +42,16 @@ struct DecArgs
 // ---------------------------------------------------------------------------
 // Wave-independent kernel: every wave owns a private LDS slot and decodes a
 // contiguous run of kRun blocks with a software pipeline: while block j is
-// decoded, the bytes of blocks j+1 and j+2 are in flight (two unconditional
-// 16-byte buffer loads per lane = up to 2 KB per block).  Three register
-// chunks rotate (loop unrolled by three) so no in-flight load result is ever
-// copied (a copy forces s_waitcnt vmcnt(0)).  No workgroup barriers at all.
-// The run's control plane lives in vector lanes (RunPlane, p4_dec_run.h).
-// Measured and kept: runs of 16 (8: same, 32..62: -2..-5%),
-// three chunks at 7 waves/SIMD (four at 6: same); with ONE (the default
-// launch), chunks are one 16-byte load each and six are in flight.
+// decoded, the bytes of the next NC-1 blocks are in flight.  Default launch
+// (ONE): one unconditional 16-byte buffer load per lane per block (its first
+// 1 KB; a bigger block's rest is loaded at staging), NC = 6; without ONE:
+// two loads per block (a 2 KB window), NC = 3.  The NC register chunks
+// rotate (loop unrolled by NC) so no in-flight load result is ever copied
+// (a copy forces s_waitcnt vmcnt(0)).  No workgroup barriers at all.  The
+// run's control plane lives in vector lanes (RunPlaneT, p4_dec_run.h).
+// Measured and kept: runs of 16 (8: same, 32..62:
+// -2..-5%), 7 waves/SIMD; ONE/NC=6 beat two loads/NC=3 by 1-2% (C2) and
+// 2-6% (C3); deeper pipelines lose occupancy.
 template <StartMode SM, uint32_t kRun, uint32_t POL = 2, uint32_t NC = 3, int MINW = 7, bool ONE = false>
 __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
 {
