@@ -122,6 +122,24 @@ int tpf_dec_batch(int fmt, const uint8_t *d_in, uint64_t in_bytes, const uint64_
 int tpf_enc_batch(int fmt, const void *d_vals, uint64_t nblocks, unsigned n, int d1, const void *d_starts, uint64_t start0,
                   uint8_t *d_out, uint64_t out_cap, uint64_t *d_off, void *d_ws, size_t ws_bytes, void *stream);
 
+/* ---- n-variant streams --------------------------------
+ * n values of any count as floor(n/256) p4Enc256v32 blocks followed, when
+ * n % 256 != 0, by one p4Enc32 block of the remaining values: the stream a
+ * caller produces by chaining turbopfor::p4Enc256v32 over the full blocks
+ * and turbopfor::p4Enc32 over the tail (reference include/turbopfor.h:9,
+ * :33; D1: p4D1Enc256v32 / p4D1Enc32 with each block's start = the value
+ * before it, the first = start0).  d_off receives nunits + 1 byte offsets
+ * (nunits = n/256 + (n%256 != 0)); d_off[nunits] is the stream's length.
+ * Decode takes the same offsets (tpf_scan_offsets of the parts, or the
+ * encoder's) and writes exactly n values. */
+uint64_t tpf_p4nenc256v32_bound(uint64_t n);
+size_t tpf_p4nenc256v32_workspace_size(uint64_t n);
+int tpf_p4nenc256v32(const uint32_t *d_in, uint64_t n, int d1, uint32_t start0, uint8_t *d_out, uint64_t out_cap,
+                     uint64_t *d_off, void *d_ws, size_t ws_bytes, void *stream);
+size_t tpf_p4ndec256v32_workspace_size(uint64_t n);
+int tpf_p4ndec256v32(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t n, int d1, uint32_t start0,
+                     uint32_t *d_out, void *d_ws, size_t ws_bytes, uint64_t *d_err, void *stream);
+
 /* ---- host pipeline utility ----------------------------------------------
  * Copies `bytes` bytes with a kernel (16-byte non-temporal stores) instead of
  * an SDMA engine; either side may be pinned/registered host memory, at any

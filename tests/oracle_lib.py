@@ -204,3 +204,24 @@ def dec32_batch(packed, off, nb, bn, starts=None):
         rc = L.orc_d1dec32_batch(ptr(src, u8p), ptr(off, u64p), nb, bn, ptr(out, u32p), ptr(st, u32p))
     assert rc == 0, rc
     return out
+
+
+# --- n-variant streams (tpf_p4nenc256v32's layout) ---------------------------
+def encn256v32(values, d1=False, start0=0):
+    """Any n: the stream a reference caller builds by chaining p4Enc256v32 over
+    the full 256-blocks and p4Enc32 over the rest (D1: p4D1* with each block's
+    start = the value before it, the first = start0).  -> (packed, offsets)"""
+    v = np.ascontiguousarray(values, dtype=np.uint32).reshape(-1)
+    n, nf, tail = len(v), len(v) // 256, len(v) % 256
+    full = v[: nf * 256].reshape(nf, 256)
+    if d1:
+        starts = np.concatenate([[start0], full.reshape(-1)[255::256][:-1]]).astype(np.uint32) if nf else None
+        packed, off = enc256v32_batch(full, starts) if nf else (np.zeros(0, np.uint8), np.zeros(1, np.uint64))
+    else:
+        packed, off = enc256v32_batch(full) if nf else (np.zeros(0, np.uint8), np.zeros(1, np.uint64))
+    if tail:
+        prev = (int(v[nf * 256 - 1]) if nf else start0) & 0xFFFFFFFF
+        t = encode("32", v[nf * 256:], d1=d1, start=prev)
+        packed = np.concatenate([packed, np.frombuffer(t, dtype=np.uint8)])
+        off = np.concatenate([off, [int(off[-1]) + len(t)]]).astype(np.uint64)
+    return packed, off

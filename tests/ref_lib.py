@@ -64,3 +64,26 @@ def enc256v32_stream(vals2d, scalar=True):
         pos = end - base
     off[nb] = pos
     return out[:pos].copy(), off
+
+
+def encn256v32_stream(values, d1=False, start0=0, scalar=True):
+    """What a reference caller writes for n values: p4(D1)Enc256v32 while 256
+    remain, then one p4(D1)Enc32 of the rest, each call at the end pointer of
+    the previous one (D1 start = the value before the block).  -> bytes"""
+    L = lib()
+    pre = "tpref_s_" if scalar else "tpref_d_"
+    f256 = getattr(L, pre + ("p4d1enc256v32" if d1 else "p4enc256v32"))
+    f32 = getattr(L, pre + ("p4d1enc32" if d1 else "p4enc32"))
+    v = np.zeros(len(values) + 64, dtype=np.uint32)
+    v[: len(values)] = values
+    n = len(values)
+    out = np.zeros(n * 6 + 4096, dtype=np.uint8)
+    base, vp, pos, i, prev = out.ctypes.data, v.ctypes.data, 0, 0, start0 & 0xFFFFFFFF
+    while i < n:
+        m = min(256, n - i)
+        f = f256 if m == 256 else f32
+        args = [ctypes.cast(vp + 4 * i, u32p), m, ctypes.cast(base + pos, u8p)] + ([prev] if d1 else [])
+        pos = f(*args) - base
+        prev = int(v[i + m - 1])
+        i += m
+    return bytes(out[:pos])

@@ -302,6 +302,108 @@ int tpf_enc_batch(int fmt, const void * d_vals, uint64_t nblocks, unsigned n, in
     return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_enc_batch");
 }
 
+// ---- n-variant streams: floor(n/256) 256v32 blocks + one
+// p4Enc32 tail block.  Workspace: [0,256) scalars (tail start, tail error,
+// tail offsets), then the tail's scratch image (encode), then the
+// sub-call's own workspace.
+static constexpr size_t kNHead = 256;
+
+static size_t ntail_image(uint64_t) { return (tpf_enc_bound(TPF_FMT_32, 1, 256) + 255) & ~size_t(255); }
+
+uint64_t tpf_p4nenc256v32_bound(uint64_t n) { return tpf_p4enc256v32_bound(n / 256) + tpf_enc_bound(TPF_FMT_32, 1, 256); }
+
+size_t tpf_p4nenc256v32_workspace_size(uint64_t n)
+{
+    const size_t full = tpf::enc256v32_workspace(n / 256), tail = tpf_enc_workspace_size(TPF_FMT_32, 1, 256);
+    return kNHead + ntail_image(n) + (full > tail ? full : tail);
+}
+
+int tpf_p4nenc256v32(const uint32_t * d_in, uint64_t n, int d1, uint32_t start0, uint8_t * d_out, uint64_t out_cap, uint64_t * d_off,
+                     void * d_ws, size_t ws_bytes, void * stream)
+{
+    if (int rc = check_device())
+        return rc;
+    if (!d_off || (n && (!d_in || !d_out || !d_ws)))
+        return fail(TPF_EINVAL, "tpf_p4nenc256v32: null pointer");
+    if (ws_bytes < tpf_p4nenc256v32_workspace_size(n))
+        return fail(TPF_EINVAL, "tpf_p4nenc256v32: workspace too small");
+    if (n && out_cap < tpf_p4nenc256v32_bound(n)) // the tail lands at an offset only the device knows
+        return fail(TPF_EINVAL, "tpf_p4nenc256v32: out_cap below tpf_p4nenc256v32_bound(n)");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint64_t nfull = n / 256;
+    const unsigned tail = static_cast<unsigned>(n % 256);
+    uint8_t * ws = static_cast<uint8_t *>(d_ws);
+    uint8_t * sub_ws = ws + kNHead + ntail_image(n);
+    const size_t sub_bytes = ws_bytes - kNHead - ntail_image(n);
+    if (nfull || !tail)
+        if (int rc = enc256v32_common(d_in, nfull, nullptr, start0, d1 != 0, d_out, out_cap, d_off, sub_ws, sub_bytes, stream,
+                                      "tpf_p4nenc256v32"))
+            return rc;
+    if (!tail)
+        return TPF_OK;
+    // D1 tail: its start is the last value of the full blocks (device) or start0
+    const uint32_t * starts = (d1 && nfull) ? d_in + nfull * 256 - 1 : nullptr;
+    if (!nfull) // the whole stream is the tail block
+        return tpf_enc_batch(TPF_FMT_32, d_in, 1, tail, d1, nullptr, start0, d_out, out_cap, d_off, sub_ws, sub_bytes, stream);
+    uint64_t * tail_off = reinterpret_cast<uint64_t *>(ws + 16);
+    uint8_t * img = ws + kNHead;
+    if (int rc = tpf_enc_batch(TPF_FMT_32, d_in + nfull * 256, 1, tail, d1, starts, start0, img, ntail_image(n), tail_off, sub_ws,
+                               sub_bytes, stream))
+        return rc;
+    hipError_t e = tpf::launch_append(d_out, img, d_off + nfull, tail_off + 1, d_off + nfull + 1, s);
+    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_p4nenc256v32");
+}
+
+size_t tpf_p4ndec256v32_workspace_size(uint64_t n) { return kNHead + tpf_p4d1dec256v32_chain_workspace_size(n / 256); }
+
+int tpf_p4ndec256v32(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t n, int d1, uint32_t start0,
+                     uint32_t * d_out, void * d_ws, size_t ws_bytes, uint64_t * d_err, void * stream)
+{
+    if (int rc = check_device())
+        return rc;
+    if (n && (!d_in || !d_off || !d_out || !d_ws))
+        return fail(TPF_EINVAL, "tpf_p4ndec256v32: null pointer");
+    if (ws_bytes < tpf_p4ndec256v32_workspace_size(n))
+        return fail(TPF_EINVAL, "tpf_p4ndec256v32: workspace too small");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint64_t nfull = n / 256;
+    const unsigned tail = static_cast<unsigned>(n % 256);
+    uint8_t * ws = static_cast<uint8_t *>(d_ws);
+    if (nfull)
+    {
+        int rc = d1 ? tpf_p4d1dec256v32_chained(d_in, in_bytes, d_off, nfull, d_out, start0, ws + kNHead, ws_bytes - kNHead, d_err, stream)
+                    : tpf_p4dec256v32_batch(d_in, in_bytes, d_off, nfull, d_out, d_err, stream);
+        if (rc)
+            return rc;
+    }
+    else if (int rc = prep_err(d_err, s))
+        return rc;
+    if (!tail)
+        return TPF_OK;
+    uint32_t * start = reinterpret_cast<uint32_t *>(ws);
+    const uint32_t * starts = nullptr;
+    if (d1)
+    {
+        if (nfull)
+            starts = d_out + nfull * 256 - 1;
+        else
+        {
+            hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(start), static_cast<int>(start0), 1, s);
+            if (e != hipSuccess)
+                return hip_fail(e, "tpf_p4ndec256v32");
+            starts = start;
+        }
+    }
+    uint64_t * tail_err = d_err ? reinterpret_cast<uint64_t *>(ws + 8) : nullptr;
+    if (int rc = tpf_dec_batch(TPF_FMT_32, d_in, in_bytes, d_off + nfull, 1, tail, d_out + nfull * 256, starts, tail_err, stream))
+        return rc;
+    if (!d_err)
+        return TPF_OK;
+    hipError_t e = tpf::launch_err_merge(reinterpret_cast<unsigned long long *>(d_err), reinterpret_cast<unsigned long long *>(tail_err),
+                                         nfull, s);
+    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_p4ndec256v32");
+}
+
 int tpf_copy_async(void * dst, const void * src, uint64_t bytes, void * stream)
 {
     if (int rc = check_device())

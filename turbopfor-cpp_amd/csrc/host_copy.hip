@@ -56,10 +56,44 @@ __global__ __launch_bounds__(256) void k_copy16(uint8_t * __restrict__ dst, cons
     }
 }
 
+// n-variant streams: append a block that was encoded into scratch at a
+// position known only on the device (the total of the blocks before it):
+// dst[*pos .. *pos + *len) = src[0 .. *len), then *pos_out = *pos + *len.
+__global__ __launch_bounds__(256) void k_append(uint8_t * __restrict__ dst, const uint8_t * __restrict__ src, const uint64_t * pos,
+                                                const uint64_t * len, uint64_t * pos_out)
+{
+    const uint64_t p = *pos, n = *len;
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x)
+        dst[p + i] = src[i];
+    if (threadIdx.x == 0)
+        *pos_out = p + n;
+}
+
+// *err = min(*err, base + *sub_err) when the sub-batch reported a block.
+__global__ void k_err_merge(unsigned long long * err, const unsigned long long * sub_err, uint64_t base)
+{
+    const unsigned long long e = *sub_err;
+    if (threadIdx.x == 0 && e != ~0ull && base + e < *err)
+        *err = base + e;
+}
+
 } // namespace tpf::dev
 
 namespace tpf
 {
+
+hipError_t launch_append(uint8_t * dst, const uint8_t * src, const uint64_t * pos, const uint64_t * len, uint64_t * pos_out,
+                         hipStream_t s)
+{
+    hipLaunchKernelGGL(dev::k_append, dim3(1), dim3(256), 0, s, dst, src, pos, len, pos_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_err_merge(unsigned long long * err, const unsigned long long * sub_err, uint64_t base, hipStream_t s)
+{
+    hipLaunchKernelGGL(dev::k_err_merge, dim3(1), dim3(64), 0, s, err, sub_err, base);
+    return hipGetLastError();
+}
 
 hipError_t launch_copy(void * dst, const void * src, uint64_t bytes, hipStream_t s)
 {

@@ -27,6 +27,11 @@ enum : int
 // Kernel copy (16-B non-temporal stores) for moving data to/from pinned host
 // memory concurrently with an SDMA copy in the other direction (host_copy.hip).
 hipError_t launch_copy(void * dst, const void * src, uint64_t bytes, hipStream_t s);
+// n-variant streams: device-positioned append of a scratch-encoded block, and
+// merging a sub-batch's error index into the caller's.
+hipError_t launch_append(uint8_t * dst, const uint8_t * src, const uint64_t * pos, const uint64_t * len, uint64_t * pos_out,
+                         hipStream_t s);
+hipError_t launch_err_merge(unsigned long long * err, const unsigned long long * sub_err, uint64_t base, hipStream_t s);
 
 size_t generic_workspace(uint64_t nblocks);
 hipError_t launch_dec_generic(int fmt, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t n,

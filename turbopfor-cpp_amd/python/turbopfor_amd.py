@@ -67,7 +67,17 @@ def lib():
                                                 c_vp, c_vp]
         L.tpf_p4d1dec256v32_chain_sums.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, ctypes.c_size_t, c_vp, c_vp, c_vp]
         L.tpf_p4d1dec256v32_chain_decode.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, ctypes.c_uint32, c_vp, c_vp, c_vp]
-        for name in ("tpf_p4dec256v32_batch", "tpf_p4d1dec256v32_batch", "tpf_p4enc256v32_batch",
+        L.tpf_p4nenc256v32_bound.argtypes = [c_u64]
+        L.tpf_p4nenc256v32_bound.restype = c_u64
+        L.tpf_p4nenc256v32_workspace_size.argtypes = [c_u64]
+        L.tpf_p4nenc256v32_workspace_size.restype = ctypes.c_size_t
+        L.tpf_p4nenc256v32.argtypes = [c_vp, c_u64, ctypes.c_int, ctypes.c_uint32, c_vp, c_u64, c_vp, c_vp,
+                                       ctypes.c_size_t, c_vp]
+        L.tpf_p4ndec256v32_workspace_size.argtypes = [c_u64]
+        L.tpf_p4ndec256v32_workspace_size.restype = ctypes.c_size_t
+        L.tpf_p4ndec256v32.argtypes = [c_vp, c_u64, c_vp, c_u64, ctypes.c_int, ctypes.c_uint32, c_vp, c_vp,
+                                       ctypes.c_size_t, c_vp, c_vp]
+        for name in ("tpf_p4nenc256v32", "tpf_p4ndec256v32", "tpf_p4dec256v32_batch", "tpf_p4d1dec256v32_batch", "tpf_p4enc256v32_batch",
                      "tpf_p4d1enc256v32_batch", "tpf_dec_batch", "tpf_enc_batch", "tpf_p4d1dec256v32_chained",
                      "tpf_p4d1dec256v32_chain_sums", "tpf_p4d1dec256v32_chain_decode", "tpf_probe256v32"):
             getattr(L, name).restype = ctypes.c_int
@@ -244,4 +254,46 @@ def dec256v32_chained(packed, offsets, nblocks, start0=0, out=None, err=None, ws
                                      ctypes.c_uint32(start0 & 0xFFFFFFFF), _ptr(ws), ws.numel(), _ptr(err),
                                      _stream(torch))
     _check(rc)
+    return out
+
+
+# ---- n-variant streams (include/turbopfor_gpu.h tpf_p4nenc256v32) ----------
+def n_units(n):
+    """Blocks in an n-value stream: n // 256 256v32 blocks + one p4Enc32 tail."""
+    return n // 256 + (1 if n % 256 else 0)
+
+
+def encn256v32(values, d1=False, start0=0):
+    """Encode any number of int32 values as the stream the reference produces
+    by chaining p4Enc256v32 over the full 256-blocks and p4Enc32 over the
+    remainder (p4D1* with d1, one list starting after start0).  Returns
+    (packed uint8 tensor, offsets int64 [n_units(n) + 1])."""
+    import torch
+
+    assert values.is_cuda and values.dtype == torch.int32
+    values = values.contiguous().view(-1)
+    n = values.numel()
+    L = lib()
+    cap = int(L.tpf_p4nenc256v32_bound(n))
+    out = torch.empty(cap, dtype=torch.uint8, device=values.device)
+    offs = torch.empty(n_units(n) + 1, dtype=torch.int64, device=values.device)
+    ws_bytes = int(L.tpf_p4nenc256v32_workspace_size(n))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=values.device)
+    _check(L.tpf_p4nenc256v32(_ptr(values), n, int(bool(d1)), ctypes.c_uint32(start0 & 0xFFFFFFFF), _ptr(out), cap,
+                              _ptr(offs), _ptr(ws), ws_bytes, _stream(torch)))
+    return out[:int(offs[-1].item())], offs
+
+
+def decn256v32(packed, offsets, n, d1=False, start0=0, out=None, err=None):
+    """Decode an n-value stream of encn256v32's layout (offsets: n_units(n)+1)."""
+    import torch
+
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=packed.device)
+    L = lib()
+    ws_bytes = int(L.tpf_p4ndec256v32_workspace_size(n))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=packed.device)
+    _check(L.tpf_p4ndec256v32(_ptr(packed), packed.numel(), _ptr(offsets), n, int(bool(d1)),
+                              ctypes.c_uint32(start0 & 0xFFFFFFFF), _ptr(out), _ptr(ws), ws_bytes, _ptr(err),
+                              _stream(torch)))
     return out
