@@ -209,6 +209,95 @@ def cpu_baseline(packed_host, off_host, nblocks, budget_s=12.0, threads=None):
     }
 
 
+def _cpu_model():
+    try:
+        return [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:
+        return "unknown"
+
+
+def _timed_reps(run, budget_s):
+    """run() returns its own seconds; one untimed call, then reps until budget_s."""
+    if run() < 0:
+        raise RuntimeError("cpu baseline run failed")
+    tot, reps, t_start = 0.0, 0, time.perf_counter()
+    while time.perf_counter() - t_start < budget_s:
+        s = run()
+        if s < 0:
+            raise RuntimeError("cpu baseline run failed")
+        tot += s
+        reps += 1
+    return tot, reps
+
+
+def cpu_baseline_d1(packed_host, off_host, starts_host, nblocks, chained, budget_s=12.0, threads=None):
+    """C3 CPU baseline: the reference library (oracle/_ref) running
+    turbopfor::p4D1Dec256v32 over the first 1/8 of the same posting-list
+    stream with `threads` std::threads -- per-block starts, or (chained) each
+    thread carrying the previous block's last value as its callers do
+    (README.md:108-123).  None when oracle/_ref is absent (not built)."""
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libtpref.so")
+    if not os.path.exists(ref_so):
+        return None
+    threads = threads or min(16, os.cpu_count() or 1)
+    nb = max(1, nblocks // 8)
+    b1 = int(off_host[nb])
+    sample = np.concatenate([packed_host[:b1], np.zeros(64, np.uint8)])
+    soff = np.ascontiguousarray(off_host[: nb + 1], dtype=np.uint64)
+    st = np.ascontiguousarray(starts_host[:nb], dtype=np.uint32)
+    out = np.empty((nb, 256), dtype=np.uint32)
+    L = ctypes.CDLL(ref_so)
+    f = L.tpref_d1dec256v32_stream_mt
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
+                  ctypes.c_int, ctypes.c_int]
+    f.restype = ctypes.c_double
+    run = lambda disp: f(sample.ctypes.data, soff.ctypes.data, st.ctypes.data, nb, out.ctypes.data, threads, disp,
+                         int(chained))
+    tot, reps = _timed_reps(lambda: run(1), budget_s)
+    stot, sreps = _timed_reps(lambda: run(0), budget_s / 3)
+    return {"value": round(nb * 256 * reps / tot / 1e9, 3), "unit": "G int32/s", "cores": threads, "kind": "reference",
+            "scalar_value": round(nb * 256 * sreps / stot / 1e9, 3),
+            "sample": f"first {nb} blocks of the same C3 stream x {reps} passes, {threads} threads, "
+                      f"turbopfor::p4D1Dec256v32 (reference AVX2 dispatch, oracle/_ref; "
+                      + ("chained through each block's last value" if chained else "per-block starts")
+                      + f") on {_cpu_model()}"}
+
+
+def cpu_baseline_rt(vals_host, nblocks, budget_s=12.0, threads=None):
+    """C4 CPU baseline: the reference library (oracle/_ref) encoding the first
+    1/16 of the same C4 values with turbopfor::p4Enc256v32 (chained through
+    the returned end pointers) and decoding them back with p4Dec256v32, on
+    `threads` std::threads.  None when oracle/_ref is absent."""
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libtpref.so")
+    if not os.path.exists(ref_so):
+        return None
+    threads = threads or min(16, os.cpu_count() or 1)
+    nb = max(1, nblocks // 16)
+    # every 16th block: the sample keeps the bw / exception-rate mix of the whole stream
+    v = np.ascontiguousarray(vals_host[::16][:nb], dtype=np.uint32)
+    slot = 1088
+    scratch = np.empty(nb * slot + 64, dtype=np.uint8)
+    off = np.empty(nb, dtype=np.uint64)
+    out = np.empty((nb, 256), dtype=np.uint32)
+    L = ctypes.CDLL(ref_so)
+    f = L.tpref_rt256v32_stream_mt
+    f.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    f.restype = ctypes.c_double
+    run = lambda disp: f(v.ctypes.data, nb, scratch.ctypes.data, slot, off.ctypes.data, out.ctypes.data, threads, disp)
+    tot, reps = _timed_reps(lambda: run(1), budget_s)
+    bad_disp = int((out != v).any(axis=1).sum())
+    stot, sreps = _timed_reps(lambda: run(0), budget_s / 3)
+    bad_scalar = int((out != v).any(axis=1).sum())
+    return {"value": round(nb * 256 * reps / tot / 1e9, 3), "unit": "G int32/s", "cores": threads, "kind": "reference",
+            "scalar_value": round(nb * 256 * sreps / stot / 1e9, 3),
+            "blocks_not_round_tripped": {"dispatch": bad_disp, "scalar": bad_scalar,
+                                         "note": "dispatch (AVX2) decode mis-reads bitmap blocks with >= 32 "
+                                                 "exceptions (SURVEY.md 8 a3)"},
+            "sample": f"every 16th block of the same C4 values ({nb} blocks) x {reps} passes, {threads} threads, "
+                      f"turbopfor::p4Enc256v32 then p4Dec256v32 (reference dispatch, oracle/_ref) on {_cpu_model()}"}
+
+
 def abtest_single_block(packed_host, off_host, nblocks):
     """SURVEY §8(d) CPU baseline (i): the ab_test methodology
     (benchmarks/ab_test.cpp:553-701) -- one block L1-hot, 1000 warm-up calls,
@@ -486,8 +575,10 @@ def run_c3(args, world, rank, dev, T, chained):
            "nblocks_per_gpu": nb, "bytes_per_int": round(pbytes / nb / 256, 4), "vbyte_block_frac": round(vb_frac, 4),
            "parallelism": f"shard{world}", "verified": ok}
     metric = "G int32/s device-resident p4D1Dec256v32" + (" (chained list)" if chained else "")
+    cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_d1(
+        packed.cpu().numpy(), offs.cpu().numpy().astype(np.uint64), starts.cpu().numpy().view(np.uint32), nb, chained)
     return line(metric, value, "G int32/s", world, args.steps, args.warmup, elapsed, "u32",
-                "synthetic (GPU-generated posting lists, GPU-encoded)", cfg, roof), ok
+                "synthetic (GPU-generated posting lists, GPU-encoded)", cfg, roof, cpu), ok
 
 
 def run_c4(args, world, rank, dev, T):
@@ -503,7 +594,7 @@ def run_c4(args, world, rank, dev, T):
         state["p"], state["o"] = p, o
         tpf.dec256v32(p, o, nb, out=dec_out)
 
-    elapsed, _ = T.run(rt, args.steps, args.warmup)
+    elapsed, rt_ms = T.run(rt, args.steps, args.warmup)
     ok = bool(torch.equal(dec_out, vals))
     # 64-bit 256v64 round trip on a quarter of the blocks
     nb64 = max(1, nb // 4)
@@ -542,8 +633,26 @@ def run_c4(args, world, rank, dev, T):
                                 "packed_bytes_per_block": round(p64 / nb64, 1),
                                 "dec_alg_GBps": round((p64 + nb64 * (2048 + 8)) / (float(np.mean(dec64_ms)) * 1e-3) / 1e9, 1),
                                 "verified": ok64}}
+    # roofline of the step (encode = plan + offset scan + write launches, then
+    # the decode launch, all on the launch stream): algorithmic bytes are the
+    # encoder's (1024 in + block out + 8 offset) plus the decoder's (block in
+    # + 1024 out + 8 offset) per block; the encoder's second read of the
+    # values (plan pass, then write pass) is not counted
+    pbytes = int(state["o"][-1].item())
+    alg_enc = nb * (1024 + 8) + pbytes + 8
+    alg_dec = pbytes + nb * (1024 + 8) + 8
+    gbs = lambda b, ms: round(b / (float(np.mean(ms)) * 1e-3) / 1e9, 1)
+    rt_gbs = gbs(alg_enc + alg_dec, rt_ms)
+    roof = {"bound": "hbm", "achieved": rt_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(rt_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "round-trip step: k_enc256v32_plan + rocprim offset scan + k_enc256v32_write + k_dec256v32w<None>",
+            "kernel_ms_avg": round(float(np.mean(rt_ms)), 4), "alg_bytes_per_launch": int(alg_enc + alg_dec),
+            "alg_bytes_def": "encode: 1024 B values + block bytes + 8 B offset; decode: block bytes + 1024 B + 8 B",
+            "enc_achieved_GBps": gbs(alg_enc, enc_ms), "enc_ms_avg": round(float(np.mean(enc_ms)), 4),
+            "dec_achieved_GBps": gbs(alg_dec, dec_ms), "dec_ms_avg": round(float(np.mean(dec_ms)), 4)}
+    cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_rt(vals.cpu().numpy().view(np.uint32), nb)
     return line("G int32/s device-resident p4Enc256v32+p4Dec256v32 round trip", value, "G int32/s", world, args.steps,
-                args.warmup, elapsed, "u32", "synthetic (GPU-generated)", cfg), ok and ok64
+                args.warmup, elapsed, "u32", "synthetic (GPU-generated)", cfg, roof, cpu), ok and ok64
 
 
 def cpu_abtest_c1(vals_host, blk_host, blen, n):

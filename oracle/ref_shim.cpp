@@ -101,6 +101,81 @@ double tpref_dec256v32_stream_mt(const uint8_t * in, const uint64_t * off, uint6
     return std::chrono::duration<double>(t1 - t0).count();
 }
 
+// Streaming p4D1Dec256v32 of nblocks blocks with their starts, the way a
+// posting-list reader calls the reference (README.md:108-123): chained != 0
+// takes starts[] only for each thread's first block and carries the previous
+// block's last value after that; chained == 0 passes starts[i] per block.
+// Returns wall seconds of the parallel region.
+double tpref_d1dec256v32_stream_mt(const uint8_t * in, const uint64_t * off, const uint32_t * starts,
+                                   uint64_t nblocks, uint32_t * out, int nthreads, int use_dispatch, int chained)
+{
+    if (nthreads < 1)
+        nthreads = 1;
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t)
+    {
+        uint64_t lo = nblocks * (uint64_t)t / (uint64_t)nthreads;
+        uint64_t hi = nblocks * (uint64_t)(t + 1) / (uint64_t)nthreads;
+        th.emplace_back([=] {
+            for (uint64_t i = lo; i < hi; ++i)
+            {
+                uint32_t * o = out + i * 256u;
+                const uint32_t st = (chained && i > lo) ? o[-1] : starts[i];
+                if (use_dispatch)
+                    turbopfor::p4D1Dec256v32(in + off[i], 256u, o, st);
+                else
+                    turbopfor::scalar::p4D1Dec256v32(in + off[i], 256u, o, st);
+            }
+        });
+    }
+    for (auto & x : th)
+        x.join();
+    auto t1 = std::chrono::steady_clock::now();
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// Round trip of nblocks blocks of 256 u32 (block i at vals + 256 i): each
+// thread encodes its contiguous range with p4Enc256v32, chaining through the
+// returned end pointers into its own slice of `scratch` (slice = range x
+// `slot` bytes) and noting each block's start in off[i], then decodes the
+// blocks back with p4Dec256v32 from off[i] (not through the decoder's end
+// pointer: the dispatch path's is wrong for bitmap blocks with >= 32
+// exceptions).  `slot` must be >= 1040 (a 256v32 block is
+// at most 1 + 32*32 bytes, plus the encoder's 4-byte over-write).  Returns
+// wall seconds of the parallel region, or -1 on a bad slot.
+double tpref_rt256v32_stream_mt(const uint32_t * vals, uint64_t nblocks, uint8_t * scratch, uint64_t slot,
+                                uint64_t * off, uint32_t * out, int nthreads, int use_dispatch)
+{
+    if (nthreads < 1)
+        nthreads = 1;
+    if (slot < 1040)
+        return -1.0;
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t)
+    {
+        uint64_t lo = nblocks * (uint64_t)t / (uint64_t)nthreads;
+        uint64_t hi = nblocks * (uint64_t)(t + 1) / (uint64_t)nthreads;
+        th.emplace_back([=] {
+            uint8_t * e = scratch + lo * slot;
+            for (uint64_t i = lo; i < hi; ++i)
+            {
+                off[i] = static_cast<uint64_t>(e - scratch);
+                uint32_t * in = const_cast<uint32_t *>(vals + i * 256u);
+                e = use_dispatch ? turbopfor::p4Enc256v32(in, 256u, e) : turbopfor::scalar::p4Enc256v32(in, 256u, e);
+            }
+            for (uint64_t i = lo; i < hi; ++i)
+                use_dispatch ? (void)turbopfor::p4Dec256v32(scratch + off[i], 256u, out + i * 256u)
+                             : (void)turbopfor::scalar::p4Dec256v32(scratch + off[i], 256u, out + i * 256u);
+        });
+    }
+    for (auto & x : th)
+        x.join();
+    auto t1 = std::chrono::steady_clock::now();
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
 // ab_test methodology (benchmarks/ab_test.cpp:553-701): one block decoded in
 // an L1-hot loop, `iters` iterations per chunk, best of `runs` runs.  Returns
 // best seconds per decode call.
