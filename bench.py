@@ -563,7 +563,7 @@ def run_c3(args, world, rank, dev, T, chained):
     probe_alg = pbytes + nb * (1024 + 8) + 8
     roof = {"bound": "hbm", "achieved": round(alg / (avg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "traffic": None if chained else pmc_traffic("c3", nb),
+            "traffic": pmc_traffic("c3chain" if chained else "c3", nb),
             "kernel_ms_avg": round(avg_ms, 4),
             "kernel": ("k_dec256v32w<SumOnly> + hipcub scan + k_dec256v32w<Prefix>" if chained
                        else "tpf::dev::k_dec256v32w<StartMode::PerBlock>"),
@@ -644,7 +644,7 @@ def run_c4(args, world, rank, dev, T):
     gbs = lambda b, ms: round(b / (float(np.mean(ms)) * 1e-3) / 1e9, 1)
     rt_gbs = gbs(alg_enc + alg_dec, rt_ms)
     roof = {"bound": "hbm", "achieved": rt_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(rt_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(rt_gbs / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("c4", nb),
             "kernel": "round-trip step: k_enc256v32_plan + rocprim offset scan + k_enc256v32_write + k_dec256v32w<None>",
             "kernel_ms_avg": round(float(np.mean(rt_ms)), 4), "alg_bytes_per_launch": int(alg_enc + alg_dec),
             "alg_bytes_def": "encode: 1024 B values + block bytes + 8 B offset; decode: block bytes + 1024 B + 8 B",

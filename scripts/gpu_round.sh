@@ -13,7 +13,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_stats -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $R/gpurun_out/bench_prof.json 2>$R/gpurun_out/bench_prof.err || { echo "rocprof rc=$?"; tail -20 $R/gpurun_out/bench_prof.err; exit 1; }
 cat $R/gpurun_out/bench_prof.json
 rm -f $R/gpurun_out/pmc_traffic.json
-for w in c2 c3 c1; do
+for w in c2 c3 c1 c3chain c4; do
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $c -d $R/gpurun_out/pmc_${w}_$c -o run --output-format csv -- python3 $R/bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline > $R/gpurun_out/bench_pmc_${w}_$c.json 2>&1 || { echo "pmc $w $c rc=$?"; tail -20 $R/gpurun_out/bench_pmc_${w}_$c.json; exit 1; }
   done

@@ -11,14 +11,25 @@ import os
 import statistics
 import sys
 
-# workload -> (kernel name test, description); names appear demangled or mangled
+def _dec(mode):
+    return lambda n: "k_dec256v32w" in n and (f"StartModeE{mode}E" in n or f"StartMode){mode}," in n)
+
+
+# workload -> (kernel name tests, description): one test per kernel of the
+# step; a step's traffic is the sum of each kernel's per-launch median.
+# Names appear demangled or mangled.
 KERNELS = {
-    "c2": (lambda n: "k_dec256v32w" in n and ("StartModeE0E" in n or "StartMode)0," in n),
-           "tpf::dev::k_dec256v32w<StartMode::None>"),
-    "c3": (lambda n: "k_dec256v32w" in n and ("StartModeE1E" in n or "StartMode)1," in n),
-           "tpf::dev::k_dec256v32w<StartMode::PerBlock>"),
-    "c1": (lambda n: "k_dec_gr" in n and ("FmtE0E" in n or "Fmt)0," in n),
-           "tpf::dev::k_dec_gr<Fmt::H32>"),
+    "c2": ([_dec(0)], "tpf::dev::k_dec256v32w<StartMode::None>"),
+    "c3": ([_dec(1)], "tpf::dev::k_dec256v32w<StartMode::PerBlock>"),
+    "c1": ([lambda n: "k_dec_gr" in n and ("FmtE0E" in n or "Fmt)0," in n)], "tpf::dev::k_dec_gr<Fmt::H32>"),
+    # chained list: phase A (block sums) + phase B (prefix decode); the
+    # hipcub scan of 10M u32 sums between them (~80 MB) is not counted
+    "c3chain": ([_dec(3), _dec(2)], "k_dec256v32w<SumOnly> + k_dec256v32w<Prefix>"),
+    # round trip: encoder plan + write passes (non-D1) + decode; the rocprim
+    # offset scan (10M u64, ~0.16 GB) is not counted
+    "c4": ([lambda n: "k_enc256v32_plan" in n and ("ILb0E" in n or "<false" in n),
+            lambda n: "k_enc256v32_write" in n and ("ILb0E" in n or "<false" in n), _dec(0)],
+           "k_enc256v32_plan<false> + k_enc256v32_write<false> + k_dec256v32w<StartMode::None>"),
 }
 
 
@@ -32,9 +43,15 @@ def per_launch(path, counter, test):
 
 def main():
     wl, fetch_csv, write_csv, nblocks, out = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5]
-    test, kname = KERNELS[wl]
-    f_kib, nf = per_launch(fetch_csv, "FETCH_SIZE", test)
-    w_kib, nw = per_launch(write_csv, "WRITE_SIZE", test)
+    tests, kname = KERNELS[wl]
+    f_kib = w_kib = 0.0
+    nf, nw = [], []
+    for test in tests:
+        f, a = per_launch(fetch_csv, "FETCH_SIZE", test)
+        w, b = per_launch(write_csv, "WRITE_SIZE", test)
+        f_kib, w_kib = f_kib + f, w_kib + w
+        nf.append(a)
+        nw.append(b)
     hbm = (2.0 * f_kib + w_kib) * 1024.0
     d = {"workload": wl, "nblocks": nblocks, "kernel": kname,
          "FETCH_SIZE_KiB_median": f_kib, "WRITE_SIZE_KiB_median": w_kib, "launches": [nf, nw],
