@@ -40,7 +40,10 @@ __device__ __forceinline__ uint32_t vblen32(uint32_t x)
 }
 
 // hist: per-wave LDS scratch of kPlanHistU32 u32 (16-byte aligned).
-using PlanHist = WaveHist<16, 36>; // bit widths 0..32
+// 4 copies: the plan pass is bound by its LDS traffic as much as by conflicts
+// (A/B, C4 encode: 16 copies 447-451 G int32/s, 32 copies 337, 8 copies 454,
+// 4 copies 453-457; merging equal widths within a lane first: no gain)
+using PlanHist = WaveHist<4, 36>; // bit widths 0..32
 constexpr uint32_t kPlanHistU32 = PlanHist::kU32;
 __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist, uint32_t t)
 {
