@@ -205,7 +205,7 @@ __global__ __launch_bounds__(256) void k_enc256v32_write(const uint32_t * __rest
             wave_lds_sync();
             return;
         }
-        const uint32_t sb = emit_block256(img, val_all[wv], P, v, t);
+        const uint32_t sb = emit_block256<true>(img, val_all[wv], P, v, t);
         wave_lds_sync();
         copy_out_image16(img, sb, dst, size, cap_end, t);
         wave_lds_sync();

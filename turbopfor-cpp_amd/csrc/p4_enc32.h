@@ -168,7 +168,17 @@ __device__ __forceinline__ void or_bits(uint32_t * img, uint32_t bp, uint32_t va
 // 162 SALU + 51 LDS-conflict cycles per block); a per-dword gather variant
 // was slower still (dependent LDS reads, 7.4 ms per 10M blocks).
 
-constexpr uint32_t kEncValU32 = 256; // staged masked base values, element order
+// staged masked base values, element e at val_idx(e): with PAD, 4 dwords of
+// padding after every 32 elements, so pack_base_runs' column reads (lane
+// 8l + r reads element 32r + l + 8j, ds_read_b32 banks (a/4) % 32 per 32-lane
+// half) land on 32 distinct banks instead of 8-way on 4 (A/B, C4 encode:
+// 455-458 -> 460-464 G int32/s)
+constexpr uint32_t kEncValU32 = 256 + 32;
+template <bool PAD>
+__device__ __forceinline__ uint32_t val_idx(uint32_t e)
+{
+    return PAD ? e + 4u * (e >> 5) : e;
+}
 // Block images start at byte kImgLead..kImgLead+3 (the payload lands on a
 // dword); the 16-byte lead lets copy_out_image16 address the first chunk
 // before the block without going below the image.
@@ -219,18 +229,20 @@ __device__ __forceinline__ uint32_t run_maxw(uint32_t cnt, uint32_t nb) { return
 // Base payload (256v32 layout) at image dword pw from the staged values:
 // word (k, l) at img[pw + 8k + l] holds bits [32k, 32k+32) of column l,
 // whose g-th value is element 8g + l.
+template <bool PAD>
 __device__ __forceinline__ void pack_base_runs(uint32_t * img, uint32_t pw, const uint32_t * val, uint32_t b, uint32_t t)
 {
     if (b == 0u)
         return;
     const uint32_t l = t >> 3, r = t & 7u;
-    const uint32_t e = 32u * r + l; // element of group 4r in column l
+    const uint32_t e = val_idx<PAD>(32u * r + l); // element of group 4r in column l
     const uint32_t x[4] = {val[e], val[e + 8u], val[e + 16u], val[e + 24u]};
     or_run(img, pw + l, 8u, 4u * r * b, x, 4u, b, run_maxw(4u, b));
 }
 
 // Build block image; returns sb (image byte of the block's first byte).
 // v: lane t's values 4t..4t+3 (after delta coding), P: plan, val: scratch.
+template <bool PAD = false>
 __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val, const Plan32 & P, const u32x4 & v,
                                                   uint32_t t)
 {
@@ -251,13 +263,13 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
     const uint32_t po = P.bx == 0u ? 1u : (P.bx <= 32u ? 34u + xbytes : 2u); // payload offset in the block
     const uint32_t sb = kImgLead + ((4u - (po & 3u)) & 3u);
     const uint32_t pw = (sb + po) >> 2;
-    reinterpret_cast<u32x4 *>(val)[t] = u32x4{v.x & m, v.y & m, v.z & m, v.w & m};
+    *reinterpret_cast<u32x4 *>(val + val_idx<PAD>(4u * t)) = u32x4{v.x & m, v.y & m, v.z & m, v.w & m};
     if (P.bx == 0u)
     {
         if (t == 0)
             ib[sb] = static_cast<uint8_t>(b);
         wave_lds_sync();
-        pack_base_runs(img, pw, val, b, t);
+        pack_base_runs<PAD>(img, pw, val, b, t);
         return sb;
     }
     const uint32_t f0 = v.x > m, f1 = v.y > m, f2 = v.z > m, f3 = v.w > m;
@@ -279,7 +291,7 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
         if ((t & 1u) == 0u)
             ib[sb + 2u + (t >> 1)] = static_cast<uint8_t>(my | (mynext << 4));
         wave_lds_sync();
-        pack_base_runs(img, pw, val, b, t);
+        pack_base_runs<PAD>(img, pw, val, b, t);
         // this lane's exceptions are the consecutive ranks before..before+cnt-1
         // compact the flagged values to the front, in order (selects only)
         uint32_t xr[4] = {0u, 0u, 0u, 0u};
@@ -303,7 +315,7 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
         ib[sb + 1u] = static_cast<uint8_t>(P.xn);
     }
     wave_lds_sync();
-    pack_base_runs(img, pw, val, b, t);
+    pack_base_runs<PAD>(img, pw, val, b, t);
     const uint32_t v0 = sb + 2u + 32u * b;
     if (P.raw)
     {
