@@ -626,7 +626,7 @@ def run_c4(args, world, rank, dev, T):
     g = lambda n, ms: round(n * 256 / (float(np.mean(ms)) * 1e-3) / 1e9, 2)
     p64 = int(st64["p"].numel())
     cfg = {"workload": "C4: p4Enc256v32 + p4Dec256v32 round trip, bw 1..32 segments cycling 0/5/10/25% exceptions",
-           "nblocks_per_gpu": nb, "verified": ok,
+           "nblocks_per_gpu": nb, "parallelism": f"shard{world}", "verified": ok,
            "enc256v32_G_int32_per_s": g(nb, enc_ms), "dec256v32_G_int32_per_s": g(nb, dec_ms),
            "roundtrip_256v64": {"nblocks": nb64, "G_int64_per_s": round(nb64 * 256 / (el64 / s64) / 1e9, 2),
                                 "enc_G_int64_per_s": g(nb64, enc64_ms), "dec_G_int64_per_s": g(nb64, dec64_ms),
