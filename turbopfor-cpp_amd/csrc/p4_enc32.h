@@ -60,8 +60,8 @@ __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist
     }
     const uint32_t maxb = bw32(orv);
     const uint32_t first = __builtin_amdgcn_readlane(v.x, 0);
-    const uint32_t eqc = wave_sum((v.x == first) + (v.y == first) + (v.z == first) + (v.w == first));
-    if (eqc == 256u)
+    // constant block: a ballot, not a wave reduction
+    if (__builtin_amdgcn_ballot_w64(!((v.x == first) & (v.y == first) & (v.z == first) & (v.w == first))) == 0ull)
     {
         P.b = maxb;
         P.bx = 34;
@@ -117,30 +117,31 @@ __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist
     }
     const uint32_t b = P.b;
     const uint32_t m = mask32(b);
-    // exception count (low half) and, for vbyte, their vbyte bytes (high
-    // half, <= 5*256) in one reduction
-    uint32_t cl = (v.x > m) + (v.y > m) + (v.z > m) + (v.w > m);
-    if (kind != 0u)
-        cl |= ((v.x > m ? vblen32(v.x >> b) : 0u) + (v.y > m ? vblen32(v.y >> b) : 0u) + (v.z > m ? vblen32(v.z >> b) : 0u)
-               + (v.w > m ? vblen32(v.w >> b) : 0u))
-            << 16;
-    const uint32_t tot = wave_sum(cl);
-    const uint32_t xn = tot & 0xFFFFu;
-    P.xn = xn;
     if (kind == 0u)
     {
+        // bitmap patch: xn = ec(b), already in lane b (no second reduction;
+        // A/B with the constant-test ballot: C4 encode 459-462 -> 463-466)
+        const uint32_t xn = uni(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ec), static_cast<int>(b))));
+        P.xn = xn;
         P.bx = maxb - b;
         P.size = 34u + ((xn * P.bx + 7u) >> 3) + 32u * b;
         P.raw = 0;
+        return P;
     }
-    else
-    {
-        P.bx = 33;
-        const uint32_t sumlen = tot >> 16;
-        P.raw = (sumlen + 32u > 4u * xn) ? 1u : 0u;
-        const uint32_t vsize = P.raw ? 1u + 4u * xn : sumlen;
-        P.size = 2u + 32u * b + vsize + xn;
-    }
+    // vbyte: exception count (low half) and their vbyte bytes (high half,
+    // <= 5*256) in one reduction
+    const uint32_t cl = (v.x > m) + (v.y > m) + (v.z > m) + (v.w > m)
+                        + (((v.x > m ? vblen32(v.x >> b) : 0u) + (v.y > m ? vblen32(v.y >> b) : 0u)
+                            + (v.z > m ? vblen32(v.z >> b) : 0u) + (v.w > m ? vblen32(v.w >> b) : 0u))
+                           << 16);
+    const uint32_t tot = wave_sum(cl);
+    const uint32_t xn = tot & 0xFFFFu;
+    P.xn = xn;
+    P.bx = 33;
+    const uint32_t sumlen = tot >> 16;
+    P.raw = (sumlen + 32u > 4u * xn) ? 1u : 0u;
+    const uint32_t vsize = P.raw ? 1u + 4u * xn : sumlen;
+    P.size = 2u + 32u * b + vsize + xn;
     return P;
 }
 
