@@ -394,11 +394,12 @@ __device__ __forceinline__ PlanG plan_block_g(const typename FmtTraits<F>::T v[4
     }
     const uint32_t maxb = bw64d(orv);
     const uint64_t first = readlane64(static_cast<uint64_t>(v[0]), 0);
-    uint32_t eqc = 0;
+    // constant block: a ballot, not a wave reduction
+    bool same = true;
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j)
-        eqc += (t + 64u * j < n && static_cast<uint64_t>(v[j]) == first) ? 1u : 0u;
-    if (wave_sum(eqc) == n)
+        same = same && (t + 64u * j >= n || static_cast<uint64_t>(v[j]) == first);
+    if (__builtin_amdgcn_ballot_w64(!same) == 0ull)
     {
         P.b = maxb;
         P.bx = W + 2u;
@@ -449,6 +450,16 @@ __device__ __forceinline__ PlanG plan_block_g(const typename FmtTraits<F>::T v[4
         P.size = 1u + base_bytes<F>(NE, b);
         return P;
     }
+    P.b = b;
+    if ((kmin & 1u) == 0u)
+    {
+        // bitmap patch: xn = ec(b), already in lane b (b <= 63 here)
+        const uint32_t xn = uni(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ec), static_cast<int>(b))));
+        P.xn = xn;
+        P.bx = maxb - b;
+        P.size = 2u + bmp + pad8d(xn * P.bx) + base_bytes<F>(NE, b);
+        return P;
+    }
     const uint64_t m = mask64d(b);
     uint32_t xc = 0, sl = 0;
 #pragma unroll
@@ -461,21 +472,12 @@ __device__ __forceinline__ PlanG plan_block_g(const typename FmtTraits<F>::T v[4
         }
     const uint32_t xs_tot = wave_sum(xc | (sl << 16)); // count | vbyte bytes (<= 9*256)
     const uint32_t xn = xs_tot & 0xFFFFu;
-    P.b = b;
     P.xn = xn;
-    if ((kmin & 1u) == 0u)
-    {
-        P.bx = maxb - b;
-        P.size = 2u + bmp + pad8d(xn * P.bx) + base_bytes<F>(NE, b);
-    }
-    else
-    {
-        P.bx = W + 1u;
-        const uint32_t sumlen = xs_tot >> 16;
-        constexpr uint32_t ES = W / 8u;
-        P.raw = (sumlen + 32u > ES * xn) ? 1u : 0u;
-        P.size = 2u + base_bytes<F>(NE, b) + (P.raw ? 1u + ES * xn : sumlen) + xn;
-    }
+    P.bx = W + 1u;
+    const uint32_t sumlen = xs_tot >> 16;
+    constexpr uint32_t ES = W / 8u;
+    P.raw = (sumlen + 32u > ES * xn) ? 1u : 0u;
+    P.size = 2u + base_bytes<F>(NE, b) + (P.raw ? 1u + ES * xn : sumlen) + xn;
     return P;
 }
 
