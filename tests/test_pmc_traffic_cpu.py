@@ -1,0 +1,56 @@
+"""scripts/pmc_traffic.py (roofline.traffic source): per-launch medians of
+FETCH_SIZE / WRITE_SIZE, FETCH doubled per the gfx950 correction, summed over
+every kernel of a multi-kernel step (c3chain, c4), merged into one JSON file
+per workload.  Synthetic rocprofv3 CSVs; no GPU."""
+import csv
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCRIPT = os.path.join(ROOT, "scripts", "pmc_traffic.py")
+
+
+def _csv(path, counter, rows):
+    with open(path, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Kernel_Name", "Counter_Name", "Counter_Value"])
+        w.writeheader()
+        for name, val in rows:
+            w.writerow({"Kernel_Name": name, "Counter_Name": counter, "Counter_Value": val})
+
+
+def _run(tmp_path, wl, fetch_rows, write_rows, out):
+    f, w = tmp_path / f"{wl}_f.csv", tmp_path / f"{wl}_w.csv"
+    _csv(f, "FETCH_SIZE", fetch_rows)
+    _csv(w, "WRITE_SIZE", write_rows)
+    subprocess.run([sys.executable, SCRIPT, wl, str(f), str(w), "1000", str(out)], check=True,
+                   capture_output=True)
+    return json.load(open(out))[wl]
+
+
+DEC0 = "void tpf::dev::k_dec256v32w<(tpf::dev::StartMode)0, 16u, 2u, 6u, 7, true>(tpf::dev::DecArgs)"
+PLAN = "void tpf::dev::k_enc256v32_plan<false, 0>(unsigned int const*, unsigned long)"
+WRITE = "void tpf::dev::k_enc256v32_write<false, 0>(unsigned int const*, unsigned long)"
+PLAN_D1 = "void tpf::dev::k_enc256v32_plan<true, 0>(unsigned int const*, unsigned long)"
+
+
+def test_single_kernel_median_and_correction(tmp_path):
+    out = tmp_path / "t.json"
+    d = _run(tmp_path, "c2", [(DEC0, 10), (DEC0, 30), (DEC0, 20), ("other_kernel", 999)],
+             [(DEC0, 5), (DEC0, 5), (DEC0, 7)], out)
+    assert d["FETCH_SIZE_KiB_median"] == 20 and d["WRITE_SIZE_KiB_median"] == 5
+    assert d["hbm_bytes_per_launch"] == (2 * 20 + 5) * 1024
+
+
+def test_step_sums_its_kernels_and_merges(tmp_path):
+    out = tmp_path / "t.json"
+    _run(tmp_path, "c2", [(DEC0, 1)], [(DEC0, 1)], out)
+    d = _run(tmp_path, "c4",
+             [(PLAN, 100), (PLAN, 100), (WRITE, 200), (DEC0, 50), (PLAN_D1, 7777)],
+             [(PLAN, 1), (WRITE, 60), (DEC0, 100), (PLAN_D1, 7777)], out)
+    # the D1 plan kernel is not part of the C4 step
+    assert d["FETCH_SIZE_KiB_median"] == 350 and d["WRITE_SIZE_KiB_median"] == 161
+    assert d["hbm_bytes_per_launch"] == (2 * 350 + 161) * 1024
+    both = json.load(open(out))
+    assert set(both) == {"c2", "c4"}
