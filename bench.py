@@ -17,13 +17,19 @@ Other workloads (--workload, one JSON line each, for DESIGN.md):
   c3chain the same list decoded as ONE chained list (only start0 given)
   c4      p4Enc256v32 + p4Dec256v32 round trip (0/5/10/25% exceptions) and
           the 256v64 round trip (bw 1..64 with exceptions above bit 32)
+  sweep   SURVEY §8(d): 10M blocks for EACH bit width 1..32, decode vs probe
 --e2e adds the host-memory rates (pinned H2D + decode + D2H, tpf_host_dec; and
       the encode trip, tpf_host_enc).
 
-Multi-GPU (torchrun, one process per GPU): every rank owns its own shard
-(weak scaling); the decode needs no collective.  RCCL carries the barrier,
-the max-over-ranks time and, for c3chain, the one real exchange step (each
-shard's delta total, tpf_shard.chained_base).
+Multi-GPU: `python bench.py --gpus N` (N > 1, WORLD_SIZE unset) starts
+`torch.distributed.run` with N ranks as a child process before anything
+touches a GPU and exits with its status; under a launcher (WORLD_SIZE set)
+every rank owns its own shard (weak scaling); the decode needs no
+collective.  RCCL carries the barrier, the max-over-ranks time, the per-rank
+kernel times and, for c3chain, the one real exchange step (each shard's delta
+total, tpf_shard.chained_base).  --selftest runs the same launcher, process
+group and timing plumbing with a CPU stand-in step (gloo; no GPU, no codec)
+for the CPU tests.
 
 Rank 0 prints ONE JSON line with `roofline` (decode kernel, HIP events on
 the launch stream) and `cpu_baseline` (the reference library compiled from
@@ -31,8 +37,11 @@ its own sources, run on this host's cores on a bounded sample).
 """
 import argparse
 import ctypes
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -85,6 +94,27 @@ def gen_c2(nblocks, exc_pct, seed, dev, pcts=None):
     return vals, seg
 
 
+def gen_bw(nblocks, bw, exc_pct, seed, dev):
+    """[nblocks, 256] uint32 bit patterns of ONE bit width (C2's per-width
+    generator, benchmarks/ab_test.cpp:1606-1632), generated in 64M-value parts."""
+    vals = torch.empty((nblocks, 256), dtype=torch.int32, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed * 1000 + bw)
+    flat = vals.view(-1)
+    step = 64 << 20
+    for a in range(0, flat.numel(), step):
+        n = min(step, flat.numel() - a)
+        v = torch.randint(0, 1 << bw, (n,), device=dev, generator=g, dtype=torch.int64)
+        if exc_pct > 0 and bw <= 28:
+            m = torch.rand(n, device=dev, generator=g) < (exc_pct / 100.0)
+            e = torch.randint(1 << bw, 1 << 32, (n,), device=dev, generator=g, dtype=torch.int64)
+            v = torch.where(m, e, v)
+            del m, e
+        flat[a:a + n] = as_i32(v)
+        del v
+    return vals
+
+
 def gen_c3(nblocks, seed, dev):
     """Sorted posting list: 95% gaps bounded Zipf(s=1.1) on [1,64], 5% gaps
     64+U[0,2^16).  Returns values [nblocks,256] (int32 bit
@@ -114,28 +144,113 @@ def gen_c3(nblocks, seed, dev):
 
 
 # --------------------------------------------------------- profile traffic
-def pmc_traffic(workload, nblocks):
-    """HBM bytes per decode launch measured with rocprofv3 PMC counters for
-    exactly this workload (profiles/pmc_traffic.json, written by
-    scripts/pmc_traffic.py: FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM
-    plus WRITE_SIZE, KiB -> bytes).  None when no matching measurement."""
+def lib_md5():
     try:
-        d = json.load(open(PROFILE_TRAFFIC))
+        return hashlib.md5(open(tpf.LIB_PATH, "rb").read()).hexdigest()
+    except OSError:
+        return None
+
+
+def pmc_traffic(workload, nblocks):
+    """(HBM bytes per step, source) from rocprofv3 PMC counters of exactly this
+    workload (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py:
+    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM plus WRITE_SIZE, KiB ->
+    bytes).  PMC counters need a rocprofv3 pass of their own, so the number is
+    never measured inside this run: it is replayed only when the entry was
+    taken with the very library this process loaded (md5), and the source
+    says which measurement it is.  (None, reason) otherwise."""
+    src = {"file": os.path.relpath(PROFILE_TRAFFIC, ROOT), "measured_in_this_run": False}
+    try:
+        d = json.load(open(PROFILE_TRAFFIC)).get(workload, {})
     except Exception:
-        return None
-    d = d.get(workload, {}) if "workload" not in d else d
+        d = {}
     if d.get("workload") != workload or int(d.get("nblocks", -1)) != nblocks:
-        return None
-    return d.get("hbm_bytes_per_launch")
+        src["note"] = "no PMC measurement of this workload and size"
+        return None, src
+    src.update({"label": d.get("label"), "lib_md5": d.get("lib_md5")})
+    if d.get("lib_md5") != lib_md5():
+        src["note"] = "PMC measurement taken with another build of the library: not replayed"
+        return None, src
+    src["note"] = "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this workload with this library (scripts/gpu_pmc_steps.sh)"
+    return d.get("hbm_bytes_per_launch"), src
+
+
+def traffic_fields(workload, nblocks):
+    t, src = pmc_traffic(workload, nblocks)
+    return {"traffic": t, "traffic_source": src}
+
+
+def hbm_probes(dev, nbytes=4 << 30):
+    """The box's own streaming ceilings, measured in this run with the
+    library's probe kernels (tpf_probe_hbm: 16-B non-temporal read / write /
+    copy, grid-stride): bytes moved (read + written) per second."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    a.fill_(1)
+    res = {}
+    for kind, moved in (("read", nbytes), ("write", nbytes), ("copy", nbytes)):
+        n = nbytes if kind != "copy" else nbytes // 2
+        src, dst = (a, b)
+        for _ in range(2):
+            tpf.probe_hbm(kind, dst, src, n)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            tpf.probe_hbm(kind, dst, src, n)
+        e1.record()
+        torch.cuda.synchronize()
+        res[kind + "_GBps"] = round(moved * 5 / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+    del a, b
+    res["def"] = ("tpf_probe_hbm over 4 GiB: read-only / write-only / copy (copy counts read + written bytes), "
+                  "16-B lanes, non-temporal, 128 WG/CU")
+    return res
 
 
 # ------------------------------------------------------------- cpu baseline
+def _cgroup_cpus():
+    """CPUs granted by the cgroup (cpu.max quota / period), or None."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                return float(q) / float(per)
+        except Exception:
+            pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return q / per
+    except Exception:
+        pass
+    return None
+
+
+def cpu_host():
+    """Threads for the CPU baselines: every CPU this process may run on
+    (sched_getaffinity), capped by the cgroup CPU quota when one is set (more
+    threads than the quota only queue), and the facts behind the choice."""
+    aff = len(os.sched_getaffinity(0))
+    quota = _cgroup_cpus()
+    threads = aff if quota is None else max(1, min(aff, int(quota)))
+    return threads, {"nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+                     "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"), "model": _cpu_model(),
+                     "threads_used": threads}
+
+
 def cpu_baseline(packed_host, off_host, nblocks, budget_s=12.0, threads=None):
     """Reference library (oracle/_ref: the reference's own sources compiled by
-    oracle/Makefile; turbopfor::p4Dec256v32 = its AVX2 dispatch path) decoding
-    a bounded sample of the same packed stream with `threads` std::threads.
-    Falls back to the oracle restatement (kind "port") if _ref is absent."""
-    threads = threads or min(16, os.cpu_count() or 1)
+    oracle/Makefile) decoding a bounded sample of the same packed stream with
+    `threads` std::threads.  `value` is its bit-exact scalar path
+    (turbopfor::scalar::p4Dec256v32, the parity oracle); the AVX2 dispatch
+    path (turbopfor::p4Dec256v32) is a labelled side number: it mis-decodes
+    bitmap blocks with >= 32 exceptions (src/simd/p4dec256v32.cpp:71-83,
+    SURVEY.md 8 a3).  Falls back to the oracle restatement (kind "port")
+    if _ref is absent."""
+    if threads is None:
+        threads, host = cpu_host()
+    else:
+        host = {"threads_used": threads}
     seg = [(nblocks * s) // 32 for s in range(33)]
     parts, offs = [], [np.zeros(1, dtype=np.uint64)]
     base = 0
@@ -158,10 +273,10 @@ def cpu_baseline(packed_host, off_host, nblocks, budget_s=12.0, threads=None):
         f.argtypes = [u8p, u64p, ctypes.c_uint64, u32p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         f.restype = ctypes.c_double
 
-        def run():
-            return f(sample.ctypes.data_as(u8p), soff.ctypes.data_as(u64p), nb, out.ctypes.data_as(u32p), threads, 1, 0)
+        def run():  # scalar: the bit-exact reference path
+            return f(sample.ctypes.data_as(u8p), soff.ctypes.data_as(u64p), nb, out.ctypes.data_as(u32p), threads, 0, 0)
 
-        kind, what = "reference", "turbopfor::p4Dec256v32 (reference AVX2 dispatch, oracle/_ref)"
+        kind, what = "reference", "turbopfor::scalar::p4Dec256v32 (reference scalar, bit-exact, oracle/_ref)"
     else:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib
@@ -182,30 +297,31 @@ def cpu_baseline(packed_host, off_host, nblocks, budget_s=12.0, threads=None):
         tot += run()
         reps += 1
     value = nb * 256 * reps / tot / 1e9
-    try:
-        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
-    except Exception:
-        model = "unknown"
     abt = abtest_single_block(packed_host, off_host, nblocks) if kind == "reference" else None
-    scalar = None
+    avx2 = None
     if kind == "reference":
-        # the reference's scalar path (the parity oracle) over the same sample, shorter budget
+        # the reference's AVX2 dispatch path over the same sample, shorter budget
         fs = L.tpref_dec256v32_stream_mt
-        fs(sample.ctypes.data_as(u8p), soff.ctypes.data_as(u64p), nb, out.ctypes.data_as(u32p), threads, 0, 0)
+        exp = out.copy()
+        fs(sample.ctypes.data_as(u8p), soff.ctypes.data_as(u64p), nb, out.ctypes.data_as(u32p), threads, 1, 0)
+        bad = int((out != exp).any(axis=1).sum())
         stot, sreps, s0 = 0.0, 0, time.perf_counter()
         while time.perf_counter() - s0 < budget_s / 3:
-            stot += fs(sample.ctypes.data_as(u8p), soff.ctypes.data_as(u64p), nb, out.ctypes.data_as(u32p), threads, 0, 0)
+            stot += fs(sample.ctypes.data_as(u8p), soff.ctypes.data_as(u64p), nb, out.ctypes.data_as(u32p), threads, 1, 0)
             sreps += 1
-        scalar = round(nb * 256 * sreps / stot / 1e9, 3)
+        avx2 = {"value": round(nb * 256 * sreps / stot / 1e9, 3), "bit_exact": bad == 0, "blocks_differing_from_scalar": bad,
+                "note": "turbopfor::p4Dec256v32 (AVX2 dispatch): mis-decodes bitmap blocks with >= 32 exceptions "
+                        "(src/simd/p4dec256v32.cpp:71-83, SURVEY.md 8 a3) -- a speed reference, not a parity one"}
     return {
         "value": round(value, 3),
         "unit": "G int32/s",
         "cores": threads,
         "kind": kind,
+        "host": host,
+        "avx2_dispatch": avx2,
         "abtest_single_block": abt,
-        "scalar_value": scalar,
         "sample": f"{nb} blocks (first 1/16 of each bw segment of the same C2 stream) x {reps} passes, "
-                  f"{threads} threads, {what} on {model}",
+                  f"{threads} threads, {what} on {host.get('model', _cpu_model())}",
     }
 
 
@@ -239,7 +355,7 @@ def cpu_baseline_d1(packed_host, off_host, starts_host, nblocks, chained, budget
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libtpref.so")
     if not os.path.exists(ref_so):
         return None
-    threads = threads or min(16, os.cpu_count() or 1)
+    threads, host = cpu_host() if threads is None else (threads, {"threads_used": threads})
     nb = max(1, nblocks // 8)
     b1 = int(off_host[nb])
     sample = np.concatenate([packed_host[:b1], np.zeros(64, np.uint8)])
@@ -253,12 +369,17 @@ def cpu_baseline_d1(packed_host, off_host, starts_host, nblocks, chained, budget
     f.restype = ctypes.c_double
     run = lambda disp: f(sample.ctypes.data, soff.ctypes.data, st.ctypes.data, nb, out.ctypes.data, threads, disp,
                          int(chained))
-    tot, reps = _timed_reps(lambda: run(1), budget_s)
-    stot, sreps = _timed_reps(lambda: run(0), budget_s / 3)
+    tot, reps = _timed_reps(lambda: run(0), budget_s)
+    exp = out.copy()
+    dtot, dreps = _timed_reps(lambda: run(1), budget_s / 3)
+    bad = int((out != exp).any(axis=1).sum())
     return {"value": round(nb * 256 * reps / tot / 1e9, 3), "unit": "G int32/s", "cores": threads, "kind": "reference",
-            "scalar_value": round(nb * 256 * sreps / stot / 1e9, 3),
+            "host": host,
+            "avx2_dispatch": {"value": round(nb * 256 * dreps / dtot / 1e9, 3), "blocks_differing_from_scalar": bad,
+                              "note": "turbopfor::p4D1Dec256v32 AVX2 dispatch (speed reference; its bitmap path is the "
+                                      "one of SURVEY.md 8 a3)"},
             "sample": f"first {nb} blocks of the same C3 stream x {reps} passes, {threads} threads, "
-                      f"turbopfor::p4D1Dec256v32 (reference AVX2 dispatch, oracle/_ref; "
+                      f"turbopfor::scalar::p4D1Dec256v32 (reference scalar, bit-exact, oracle/_ref; "
                       + ("chained through each block's last value" if chained else "per-block starts")
                       + f") on {_cpu_model()}"}
 
@@ -271,7 +392,7 @@ def cpu_baseline_rt(vals_host, nblocks, budget_s=12.0, threads=None):
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libtpref.so")
     if not os.path.exists(ref_so):
         return None
-    threads = threads or min(16, os.cpu_count() or 1)
+    threads, host = cpu_host() if threads is None else (threads, {"threads_used": threads})
     nb = max(1, nblocks // 16)
     # every 16th block: the sample keeps the bw / exception-rate mix of the whole stream
     v = np.ascontiguousarray(vals_host[::16][:nb], dtype=np.uint32)
@@ -285,17 +406,18 @@ def cpu_baseline_rt(vals_host, nblocks, budget_s=12.0, threads=None):
                   ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     f.restype = ctypes.c_double
     run = lambda disp: f(v.ctypes.data, nb, scratch.ctypes.data, slot, off.ctypes.data, out.ctypes.data, threads, disp)
-    tot, reps = _timed_reps(lambda: run(1), budget_s)
-    bad_disp = int((out != v).any(axis=1).sum())
-    stot, sreps = _timed_reps(lambda: run(0), budget_s / 3)
+    tot, reps = _timed_reps(lambda: run(0), budget_s)
     bad_scalar = int((out != v).any(axis=1).sum())
+    dtot, dreps = _timed_reps(lambda: run(1), budget_s / 3)
+    bad_disp = int((out != v).any(axis=1).sum())
     return {"value": round(nb * 256 * reps / tot / 1e9, 3), "unit": "G int32/s", "cores": threads, "kind": "reference",
-            "scalar_value": round(nb * 256 * sreps / stot / 1e9, 3),
-            "blocks_not_round_tripped": {"dispatch": bad_disp, "scalar": bad_scalar,
-                                         "note": "dispatch (AVX2) decode mis-reads bitmap blocks with >= 32 "
-                                                 "exceptions (SURVEY.md 8 a3)"},
+            "host": host,
+            "avx2_dispatch": {"value": round(nb * 256 * dreps / dtot / 1e9, 3), "blocks_not_round_tripped": bad_disp,
+                              "note": "turbopfor::p4Enc256v32 + p4Dec256v32 AVX2 dispatch: the decode mis-reads "
+                                      "bitmap blocks with >= 32 exceptions (SURVEY.md 8 a3) -- a speed reference"},
+            "blocks_not_round_tripped": bad_scalar,
             "sample": f"every 16th block of the same C4 values ({nb} blocks) x {reps} passes, {threads} threads, "
-                      f"turbopfor::p4Enc256v32 then p4Dec256v32 (reference dispatch, oracle/_ref) on {_cpu_model()}"}
+                      f"turbopfor::scalar::p4Enc256v32 then p4Dec256v32 (reference scalar, oracle/_ref) on {_cpu_model()}"}
 
 
 def abtest_single_block(packed_host, off_host, nblocks):
@@ -324,33 +446,53 @@ def abtest_single_block(packed_host, off_host, nblocks):
 class Timer:
     """K launches bracketed by barrier + synchronize; per-launch HIP events
     recorded on the launch stream (torch's current stream, which is the stream
-    handed to the C-ABI)."""
+    handed to the C-ABI).  On a CPU device (--selftest) the per-step times are
+    host clocks and there is nothing to synchronise."""
 
     def __init__(self, dist_on, dev):
         self.dist_on, self.dev = dist_on, dev
+        self.gpu = torch.device(dev).type == "cuda"
+
+    def _sync(self):
+        if self.gpu:
+            torch.cuda.synchronize()
 
     def run(self, fn, steps, warmup):
         for _ in range(warmup):
             fn()
-        torch.cuda.synchronize()
+        self._sync()
         if self.dist_on:
             torch.distributed.barrier()
-        torch.cuda.synchronize()
-        stream = torch.cuda.current_stream()
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        self._sync()
+        if self.gpu:
+            stream = torch.cuda.current_stream()
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        host = []
         t0 = time.perf_counter()
         for i in range(steps):
-            evs[i][0].record(stream)
+            if self.gpu:
+                evs[i][0].record(stream)
+            h0 = time.perf_counter()
             fn()
-            evs[i][1].record(stream)
-        torch.cuda.synchronize()
+            host.append((time.perf_counter() - h0) * 1e3)
+            if self.gpu:
+                evs[i][1].record(stream)
+        self._sync()
         if self.dist_on:
             torch.distributed.barrier()
-        torch.cuda.synchronize()
+        self._sync()
         elapsed = time.perf_counter() - t0
         if self.dist_on:
             elapsed = tpf_shard.max_over_ranks(elapsed, self.dev)
-        return elapsed, [a.elapsed_time(b) for a, b in evs]
+        return elapsed, ([a.elapsed_time(b) for a, b in evs] if self.gpu else host)
+
+
+def per_rank_stats(world, dev, kernel_ms, achieved_GBps):
+    """Every rank's average kernel time and HBM fraction (all_gather; rank 0 reports them)."""
+    mine = [float(kernel_ms), float(achieved_GBps)]
+    rows = tpf_shard.gather_floats(mine, dev) if world > 1 else [mine]
+    return [{"rank": r, "kernel_ms_avg": round(ms, 4), "achieved_GBps": round(gbs, 1),
+             "frac": round(gbs / HBM_PEAK_GBS, 4)} for r, (ms, gbs) in enumerate(rows)]
 
 
 def line(metric, value, unit, world, steps, warmup, elapsed, dtype, data, config, roofline=None, cpu=None):
@@ -394,71 +536,33 @@ def run_c2(args, world, rank, dev, T):
     if world > 1:
         ok = tpf_shard.all_ok(ok, dev)
 
-    if args.sweep and rank == 0:
-        off_host = offs.cpu().numpy()
-        for s in range(32):
-            lo, hi = seg[s], seg[s + 1]
-            sub_in = packed[int(off_host[lo]) : int(off_host[hi])]
-            sub_off = offs[lo : hi + 1] - int(off_host[lo])
-            sub_out = out[lo:hi]
-            for _ in range(2):
-                tpf.dec256v32(sub_in, sub_off, hi - lo, out=sub_out)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(10):
-                tpf.dec256v32(sub_in, sub_off, hi - lo, out=sub_out)
-            e1.record()
-            torch.cuda.synchronize()
-            ms = e0.elapsed_time(e1) / 10
-            # the segment's data-movement probe (same loads and stores, no decode)
-            e0.record()
-            for _ in range(10):
-                tpf.probe256v32(sub_in, sub_off, hi - lo, sub_out)
-            e1.record()
-            torch.cuda.synchronize()
-            pms = e0.elapsed_time(e1) / 10
-            nbytes = int(off_host[hi] - off_host[lo])
-            gint = (hi - lo) * 256 / ms / 1e6
-            gbs = (nbytes + (hi - lo) * 1032) / ms / 1e6
-            log(f"[sweep] bw={s + 1:2d} B/blk={nbytes / (hi - lo):7.1f} ms={ms:.4f} Gint/s={gint:8.1f} "
-                f"alg GB/s={gbs:7.1f} ({gbs / HBM_PEAK_GBS:.1%} of peak, {pms / ms:.1%} of probe)")
-
     e2e = None
     if args.e2e and rank == 0:
         e2e = measure_e2e(packed, offs, nb, vals)
     # data-movement ceiling of the same access pattern (same kernel, loads
     # and stores only, no decode) -- outside the timed region
     _, probe_ms = T.run(lambda: tpf.probe256v32(packed, offs, nb, out), 10, 2)
-    # STREAM-copy ceiling of this box (SURVEY §8 d): device-to-device copy of
-    # the 10 GB value array into a second buffer (read + write bytes / time)
-    # (rank 0 only, outside T.run: no collective)
-    copy_GBps = None
-    if rank == 0:
-        dst = torch.empty_like(out)
-        dst.copy_(out)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(5):
-            dst.copy_(out)
-        e1.record()
-        torch.cuda.synchronize()
-        copy_GBps = round(2 * out.numel() * 4 * 5 / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
-        del dst
-    if rank != 0:
-        return None
     avg_ms = float(np.mean(kern_ms))
     alg = pbytes + nb * (1024 + 8) + 8
     achieved = alg / (avg_ms * 1e-3) / 1e9
+    per_rank = per_rank_stats(world, dev, avg_ms, achieved)
+    # the box's streaming ceilings (SURVEY §8 d), measured here: rank 0 only,
+    # outside the timed region, after the other ranks' work is done
+    probes = None
+    if rank == 0 and not args.no_probes:
+        probes = hbm_probes(dev)
+    if rank != 0:
+        return None
     probe = alg / (float(np.mean(probe_ms)) * 1e-3) / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("c2", nb),
+            "frac": round(achieved / HBM_PEAK_GBS, 4), **traffic_fields("c2", nb),
             "kernel": "tpf::dev::k_dec256v32w<StartMode::None>", "kernel_ms_avg": round(avg_ms, 4),
             "kernel_ms_median": round(float(np.median(kern_ms)), 4), "kernel_ms_min": round(float(np.min(kern_ms)), 4),
             "alg_bytes_per_launch": int(alg),
             "alg_bytes_def": "packed block bytes + 1024 B decoded + 8 B offset per block",
             "probe_GBps": round(probe, 1), "frac_of_probe": round(achieved / probe, 4),
             "probe_def": "tpf_probe256v32: the decode kernel's own loads and stores with decoding removed",
-            "stream_copy_GBps": copy_GBps}
+            "hbm_probes": probes, "per_rank": per_rank}
     # the CPU baseline is timed at N=1 only (a reported baseline, not a per-rank cost)
     cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(packed.cpu().numpy(),
                                                                           offs.cpu().numpy().astype(np.uint64), nb)
@@ -473,6 +577,60 @@ def run_c2(args, world, rank, dev, T):
     data = ("synthetic (GPU-generated C2 values, GPU-encoded; full-size decode verified bit-exact: "
             + ("ok" if ok else "MISMATCH") + ")")
     return line(METRIC, value, "G int32/s", world, args.steps, args.warmup, elapsed, "u32", data, cfg, roof, cpu), ok
+
+
+def run_sweep(args, world, rank, dev, T):
+    """SURVEY §8(d) per-width sweep at full size: for every bit width 1..32,
+    nblocks (default 10M) blocks of that width alone (10 % exceptions for
+    bw <= 28), encoded on the GPU, decoded `steps` times (HIP events on the
+    launch stream), verified, and timed against the decode kernel's own
+    data-movement probe on the same stream.  value = all widths' integers /
+    all widths' decode time (each width weighted equally)."""
+    nb = args.nblocks
+    rows, tot_ms, tot_alg = [], 0.0, 0
+    out = torch.empty((nb, 256), dtype=torch.int32, device=dev)
+    t_start = time.perf_counter()
+    ok = True
+    for bw in range(1, 33):
+        vals = gen_bw(nb, bw, args.exc, seed=42 + rank, dev=dev)
+        packed_full, offs = tpf.enc256v32(vals)
+        packed = packed_full.clone()
+        del packed_full
+        _, kern_ms = T.run(lambda: tpf.dec256v32(packed, offs, nb, out=out), args.steps, args.warmup)
+        good = bool(torch.equal(out, vals))
+        _, probe_ms = T.run(lambda: tpf.probe256v32(packed, offs, nb, out), max(3, args.steps // 2), 1)
+        ok = ok and good
+        ms, pms = float(np.mean(kern_ms)), float(np.mean(probe_ms))
+        pbytes = packed.numel()
+        alg = pbytes + nb * (1024 + 8) + 8
+        row = {"bw": bw, "bytes_per_block": round(pbytes / nb, 1), "ms": round(ms, 4), "G_int32_per_s": round(nb * 256 / ms / 1e6, 1),
+               "alg_GBps": round(alg / ms / 1e6, 1), "frac": round(alg / ms / 1e6 / HBM_PEAK_GBS, 4),
+               "probe_ms": round(pms, 4), "frac_of_probe": round(pms / ms, 4), "verified": good}
+        rows.append(row)
+        tot_ms += ms
+        tot_alg += alg
+        if rank == 0:
+            log(f"[sweep] bw={bw:2d} B/blk={row['bytes_per_block']:7.1f} ms={ms:.4f} Gint/s={row['G_int32_per_s']:8.1f} "
+                f"alg GB/s={row['alg_GBps']:7.1f} ({row['frac']:.1%} of peak, {row['frac_of_probe']:.1%} of probe)"
+                + ("" if good else " MISMATCH"))
+        del vals, packed, offs
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        ok = tpf_shard.all_ok(ok, dev)
+    if rank != 0:
+        return None
+    value = 32 * nb * 256 * world / (tot_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(tot_alg / (tot_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(tot_alg / (tot_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+            "traffic_source": {"note": "no PMC pass for the sweep"}, "kernel": "tpf::dev::k_dec256v32w<StartMode::None>",
+            "per_bw": rows}
+    cfg = {"workload": f"C2 per-width sweep: {nb} blocks x 256 u32 for EACH bw 1..32, {args.exc:g}% exceptions for bw<=28",
+           "nblocks_per_bw": nb, "parallelism": f"shard{world}", "verified": ok}
+    res = line("G int32/s device-resident p4Dec256v32, per-width sweep (equal weight)", value, "G int32/s", world,
+               32 * args.steps, args.warmup, tot_ms * 1e-3, "u32",
+               "synthetic (GPU-generated per-width values, GPU-encoded; every width verified bit-exact)", cfg, roof, None)
+    res["wall_s"] = round(elapsed, 1)
+    return res, ok
 
 
 def measure_e2e(packed, offs, nb, vals):
@@ -555,21 +713,23 @@ def run_c3(args, world, rank, dev, T, chained):
     ok = bool(torch.equal(out, vals)) if (not chained or world == 1) else True
     # data-movement probe of the same stream (decode kernel's loads and stores, no decode)
     _, probe_ms = T.run(lambda: tpf.probe256v32(packed, offs, nb, out), 10, 2)
+    avg_ms = float(np.mean(kern_ms))
+    alg = pbytes + nb * (1024 + 8 + (0 if chained else 4)) + 8
+    per_rank = per_rank_stats(world, dev, avg_ms, alg / (avg_ms * 1e-3) / 1e9)
     if rank != 0:
         return None
     value = nb * 256 * world / (elapsed / args.steps) / 1e9
-    avg_ms = float(np.mean(kern_ms))
-    alg = pbytes + nb * (1024 + 8 + (0 if chained else 4)) + 8
     probe_alg = pbytes + nb * (1024 + 8) + 8
     roof = {"bound": "hbm", "achieved": round(alg / (avg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic("c3chain" if chained else "c3", nb),
+            **traffic_fields("c3chain" if chained else "c3", nb),
             "kernel_ms_avg": round(avg_ms, 4),
             "kernel": ("k_dec256v32w<SumOnly> + hipcub scan + k_dec256v32w<Prefix>" if chained
                        else "tpf::dev::k_dec256v32w<StartMode::PerBlock>"),
             "probe_GBps": round(probe_alg / (float(np.mean(probe_ms)) * 1e-3) / 1e9, 1),
             "ms_vs_probe": round(avg_ms / float(np.mean(probe_ms)), 3),
-            "probe_def": "tpf_probe256v32 on the same stream (loads + stores, no decode; no starts read)"}
+            "probe_def": "tpf_probe256v32 on the same stream (loads + stores, no decode; no starts read)",
+            "per_rank": per_rank}
     cfg = {"workload": "C3: p4D1Dec256v32 " + ("chained list (start0 only)" if chained else "per-block starts")
                        + ", Zipf(1.1) gaps on [1,64] + 5% 64+U[0,2^16)",
            "nblocks_per_gpu": nb, "bytes_per_int": round(pbytes / nb / 256, 4), "vbyte_block_frac": round(vb_frac, 4),
@@ -620,6 +780,9 @@ def run_c4(args, world, rank, dev, T):
     out64 = st64["out"]
     _, enc64_ms = T.run(lambda: tpf.enc_batch("256v64", v64.view(-1), nb64, 256), s64, 1)
     _, dec64_ms = T.run(lambda: tpf.dec_batch("256v64", st64["p"], st64["o"], nb64, 256, out=out64), s64, 1)
+    pbytes = int(state["o"][-1].item())
+    alg_rt = 2 * (nb * (1024 + 8) + pbytes + 8)
+    per_rank = per_rank_stats(world, dev, float(np.mean(rt_ms)), alg_rt / (float(np.mean(rt_ms)) * 1e-3) / 1e9)
     if rank != 0:
         return None
     value = nb * 256 * world / (elapsed / args.steps) / 1e9
@@ -644,12 +807,13 @@ def run_c4(args, world, rank, dev, T):
     gbs = lambda b, ms: round(b / (float(np.mean(ms)) * 1e-3) / 1e9, 1)
     rt_gbs = gbs(alg_enc + alg_dec, rt_ms)
     roof = {"bound": "hbm", "achieved": rt_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(rt_gbs / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("c4", nb),
+            "frac": round(rt_gbs / HBM_PEAK_GBS, 4), **traffic_fields("c4", nb),
             "kernel": "round-trip step: k_enc256v32_plan + rocprim offset scan + k_enc256v32_write + k_dec256v32w<None>",
             "kernel_ms_avg": round(float(np.mean(rt_ms)), 4), "alg_bytes_per_launch": int(alg_enc + alg_dec),
             "alg_bytes_def": "encode: 1024 B values + block bytes + 8 B offset; decode: block bytes + 1024 B + 8 B",
             "enc_achieved_GBps": gbs(alg_enc, enc_ms), "enc_ms_avg": round(float(np.mean(enc_ms)), 4),
-            "dec_achieved_GBps": gbs(alg_dec, dec_ms), "dec_ms_avg": round(float(np.mean(dec_ms)), 4)}
+            "dec_achieved_GBps": gbs(alg_dec, dec_ms), "dec_ms_avg": round(float(np.mean(dec_ms)), 4),
+            "per_rank": per_rank}
     cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_rt(vals.cpu().numpy().view(np.uint32), nb)
     return line("G int32/s device-resident p4Enc256v32+p4Dec256v32 round trip", value, "G int32/s", world, args.steps,
                 args.warmup, elapsed, "u32", "synthetic (GPU-generated)", cfg, roof, cpu), ok and ok64
@@ -696,15 +860,17 @@ def run_c1(args, world, rank, dev, T):
     elapsed, kern_ms = T.run(lambda: tpf.dec_batch("32", packed, offs, nb, n, out=out), args.steps, args.warmup)
     ok = bool(torch.equal(out, vals))
     _, enc_ms = T.run(lambda: tpf.enc_batch("32", vals, nb, n), max(2, args.steps // 4), 1)
-    if rank != 0:
-        return None
     pbytes = int(packed.numel())
-    value = nb * n * world / (elapsed / args.steps) / 1e9
     avg_ms = float(np.mean(kern_ms))
     alg = pbytes + nb * (n * 4 + 8) + 8
+    per_rank = per_rank_stats(world, dev, avg_ms, alg / (avg_ms * 1e-3) / 1e9)
+    if rank != 0:
+        return None
+    value = nb * n * world / (elapsed / args.steps) / 1e9
     roof = {"bound": "hbm", "achieved": round(alg / (avg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("c1", nb),
-            "kernel_ms_avg": round(avg_ms, 4), "kernel": "tpf::dev::k_dec_gr<H32> (run-pipelined horizontal p4Dec32 batch)"}
+            "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), **traffic_fields("c1", nb),
+            "kernel_ms_avg": round(avg_ms, 4), "kernel": "tpf::dev::k_dec_gr<H32> (run-pipelined horizontal p4Dec32 batch)",
+            "per_rank": per_rank}
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         blen = int(offs[1].item())
@@ -717,6 +883,44 @@ def run_c1(args, world, rank, dev, T):
                 elapsed, "u32", "synthetic (GPU-generated uniform [0,255], GPU-encoded)", cfg, roof, cpu), ok
 
 
+# ------------------------------------------------------------ launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """--gpus N > 1 without a launcher: run this script under
+    torch.distributed.run with N ranks (one per GPU) as a CHILD process --
+    nothing here has touched a GPU, and the parent never execs -- and return
+    its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[bench] launching {n} ranks: {' '.join(cmd[1:6])} ...")
+    return subprocess.call(cmd)
+
+
+def run_selftest(args, world, rank, dev, T):
+    """Launcher / process group / timing plumbing with a CPU stand-in step
+    (an integer reduction over a per-rank array; no GPU, no codec): the line
+    it prints is marked selftest and carries no throughput claim."""
+    x = torch.arange(1 << 20, dtype=torch.int64) + rank
+    elapsed, step_ms = T.run(lambda: int(x.sum()), args.steps, args.warmup)
+    per_rank = per_rank_stats(world, dev, float(np.mean(step_ms)), 0.0)
+    if rank != 0:
+        return None
+    res = line("selftest (CPU stand-in step, no codec)", 0.0, "none", world, args.steps, args.warmup, elapsed, "int64",
+               "synthetic", {"workload": "selftest", "parallelism": f"shard{world}",
+                             "world_size": torch.distributed.get_world_size() if world > 1 else 1,
+                             "backend": torch.distributed.get_backend() if world > 1 else None})
+    res["selftest"] = True
+    res["per_rank"] = per_rank
+    return res, True
+
+
 # -------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -725,31 +929,44 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--nblocks", type=int, default=10_000_000, help="blocks per GPU (shard)")
     ap.add_argument("--exc", type=float, default=10.0)
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c3chain", "c4"])
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c3chain", "c4", "sweep"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--sweep", action="store_true", help="c2: also time each bw segment (stderr table)")
     ap.add_argument("--e2e", action="store_true", help="c2: also measure the pinned host-memory path")
+    ap.add_argument("--no-probes", action="store_true", help="c2: skip the in-run HBM read/write/copy probes")
+    ap.add_argument("--selftest", action="store_true",
+                    help="launcher + process-group plumbing with a CPU stand-in step (gloo, no GPU)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     dist_on = world > 1
     # Rehearsal of the multi-rank path on a one-GPU box (never the measured
-    # configuration): TPF_BENCH_BACKEND=gloo TPF_BENCH_SAME_GPU=1 puts every
-    # rank on cuda:0 and carries the collectives over gloo.
-    backend = os.environ.get("TPF_BENCH_BACKEND", "nccl")
+    # configuration): TPF_BENCH_SAME_GPU=1 puts every rank on cuda:0;
+    # TPF_BENCH_BACKEND=gloo carries the collectives over gloo instead of RCCL.
+    backend = os.environ.get("TPF_BENCH_BACKEND", "gloo" if args.selftest else "nccl")
     if os.environ.get("TPF_BENCH_SAME_GPU") == "1":
         local = 0
-    torch.cuda.set_device(local)
-    dev = torch.device(f"cuda:{local}")
+    if args.selftest:
+        dev = torch.device("cpu")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device(f"cuda:{local}")
     if dist_on:
         if backend == "nccl":
             torch.distributed.init_process_group("nccl", device_id=dev)
         else:
             torch.distributed.init_process_group(backend)
+        assert torch.distributed.get_world_size() == args.gpus == world, "world size != --gpus"
     T = Timer(dist_on, dev)
-    if args.workload == "c1":
+    if args.selftest:
+        res = run_selftest(args, world, rank, dev, T)
+    elif args.workload == "c1":
         res = run_c1(args, world, rank, dev, T)
     elif args.workload == "c2":
         res = run_c2(args, world, rank, dev, T)
@@ -757,6 +974,8 @@ def main():
         res = run_c3(args, world, rank, dev, T, chained=False)
     elif args.workload == "c3chain":
         res = run_c3(args, world, rank, dev, T, chained=True)
+    elif args.workload == "sweep":
+        res = run_sweep(args, world, rank, dev, T)
     else:
         res = run_c4(args, world, rank, dev, T)
     ok = True

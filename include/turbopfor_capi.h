@@ -70,7 +70,11 @@ int64_t tpf_scan_offsets(int fmt, const uint8_t *in, uint64_t in_bytes, unsigned
  * hipHostMalloc (or registered) give full PCIe rate; pageable buffers are
  * registered (and mapped) for the duration of the call.  Staging buffers and
  * streams are pooled per device across calls; tpf_host_release() frees them.
- * h_off may be NULL for decode (offsets are scanned with tpf_scan_offsets).
+ * h_off may be NULL for decode (offsets are scanned with tpf_scan_offsets);
+ * given offsets must not decrease and must end at or below in_bytes
+ * (TPF_EINVAL otherwise), and a block whose parsed length disagrees with its
+ * offsets fails the call with TPF_ECORRUPT (tpf_last_error names the block).
+ * Encode fails with TPF_EINVAL when the blocks do not fit in out_cap.
  * Value arrays use the unit strides documented in turbopfor_gpu.h. */
 int tpf_host_dec(int fmt, const uint8_t *h_in, uint64_t in_bytes, const uint64_t *h_off, uint64_t nblocks, unsigned n,
                  void *h_vals, const void *h_starts);

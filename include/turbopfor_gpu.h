@@ -53,6 +53,13 @@ int tpf_p4dec256v32_batch(const uint8_t *d_in, uint64_t in_bytes, const uint64_t
 int tpf_probe256v32(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks,
                     uint32_t *d_out, void *stream);
 
+/* Measurement only (no reference counterpart): the device's own streaming
+ * ceilings, timed by bench.py in the same process as the codec.  kind 0 =
+ * read `bytes` of d_src (d_dst receives at most one 16-byte sink word), 1 =
+ * write `bytes` to d_dst, 2 = copy `bytes` from d_src to d_dst; 16-byte
+ * lanes, non-temporal, grid-stride.  bytes is rounded down to 16. */
+int tpf_probe_hbm(int kind, void *d_dst, const void *d_src, uint64_t bytes, void *stream);
+
 /* Replaces turbopfor::p4D1Dec256v32 (include/turbopfor.h:42, dispatch.cpp:97-104):
  * block i is decoded with start d_starts[i] (the value preceding the block). */
 int tpf_p4d1dec256v32_batch(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks,
@@ -81,7 +88,9 @@ int tpf_p4d1dec256v32_chain_decode(const uint8_t *d_in, uint64_t in_bytes, const
  * Replaces turbopfor::p4Enc256v32 (include/turbopfor.h:33, dispatch.cpp:70-77)
  * and p4D1Enc256v32 (:36, dispatch.cpp:79-86) for nblocks blocks of 256
  * values (d_in: nblocks*256 u32).  Writes the blocks end to end into d_out
- * (capacity out_cap bytes; tpf_p4enc256v32_bound(nblocks) always suffices)
+ * (capacity out_cap bytes, at least tpf_p4enc256v32_bound(nblocks): the
+ * sizes are only known on the device, so a smaller out_cap is rejected with
+ * TPF_EINVAL instead of risking a silently cut-off block)
  * and their byte offsets into d_off[0..nblocks] (d_off[nblocks] = total).
  * d_ws: device workspace of tpf_p4enc256v32_workspace_size(nblocks) bytes.
  * D1: d_starts[i] is the value preceding block i; with d_starts == NULL the
@@ -93,6 +102,12 @@ int tpf_p4enc256v32_batch(const uint32_t *d_in, uint64_t nblocks, uint8_t *d_out
                           void *d_ws, size_t ws_bytes, void *stream);
 int tpf_p4d1enc256v32_batch(const uint32_t *d_in, uint64_t nblocks, const uint32_t *d_starts, uint32_t start0,
                             uint8_t *d_out, uint64_t out_cap, uint64_t *d_off, void *d_ws, size_t ws_bytes, void *stream);
+/* Measurement only (no reference counterpart; the output is NOT a valid
+ * stream): the encoder's passes with the coding removed, same loads and
+ * stores.  mode 1 = plan pass reduced to a wave OR, 2 = write pass copying
+ * the staged values.  Arguments as tpf_p4enc256v32_batch. */
+int tpf_probe_enc256v32(int mode, const uint32_t *d_in, uint64_t nblocks, uint8_t *d_out, uint64_t out_cap,
+                        uint64_t *d_off, void *d_ws, size_t ws_bytes, void *stream);
 
 /* ---- every format of include/turbopfor.h, batched ----------------------
  * fmt selects the reference function family:
@@ -100,8 +115,10 @@ int tpf_p4d1enc256v32_batch(const uint32_t *d_in, uint64_t nblocks, const uint32
  *   TPF_FMT_128V32 p4{,D1}{Enc,Dec}128v32  (turbopfor.h:21-30)  n <= 128
  *   TPF_FMT_256V32 p4{,D1}{Enc,Dec}256v32  (turbopfor.h:33-42)  n <= 256 (n == 256 -> hot path)
  *   TPF_FMT_64     p4{,D1}{Enc,Dec}64      (turbopfor.h:45-54)  n = 1..256 (uint64)
- *   TPF_FMT_128V64 p4{,D1}{Enc,Dec}128v64  (turbopfor.h:57-67)  n == 128 (uint64)
- *   TPF_FMT_256V64 p4{,D1}{Enc,Dec}256v64  (turbopfor.h:69-80)  n == 256 (uint64; one unit = two 128v64 blocks)
+ *   TPF_FMT_128V64 p4{,D1}{Enc,Dec}128v64  (turbopfor.h:57-67)  n <= 128 (uint64)
+ *   TPF_FMT_256V64 p4{,D1}{Enc,Dec}256v64  (turbopfor.h:69-80)  n == 256 (uint64; one unit = two 128v64 blocks;
+ *                  the per-block turbopfor::p4*256v64 calls take any n and split it into 128v64 blocks
+ *                  of min(remaining, 128) values like the reference, p4enc256v64_scalar.cpp:15-30)
  * A batch holds nblocks units; unit i's values are at d_vals + i*stride with
  * stride = n for the horizontal formats and the layout's full width (128 or
  * 256) for the interleaved ones (the reference packs the full width).
@@ -115,6 +132,7 @@ int tpf_p4d1enc256v32_batch(const uint32_t *d_in, uint64_t nblocks, const uint32
 #define TPF_FMT_128V64 4
 #define TPF_FMT_256V64 5
 
+/* tpf_enc_batch requires out_cap >= tpf_enc_bound(fmt, nblocks, n) (TPF_EINVAL otherwise). */
 uint64_t tpf_enc_bound(int fmt, uint64_t nblocks, unsigned n);
 size_t tpf_enc_workspace_size(int fmt, uint64_t nblocks, unsigned n);
 int tpf_dec_batch(int fmt, const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks, unsigned n,

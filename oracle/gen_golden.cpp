@@ -354,6 +354,109 @@ static void gen64(Writer & w, uint64_t seed, bool v128)
     }
 }
 
+// n below the layout width (128v64 n < 128, 256v64 n < 256).  The reference
+// leaves the base slots past n of an exception block, and the delta slots
+// past n of a D1 block, uninitialised (p4enc128v64_scalar.cpp:59,
+// p4d1enc256v64_scalar.cpp:12): those payload bits are whatever its stack
+// held.  Each vector is encoded after zero-filling the stack (the convention
+// the oracle and the GPU path implement: padding slots are 0) and again after
+// filling it with 0xA5; where the two differ the record carries flag 4
+// ("padding bits follow the zero convention, not pinned by the reference").
+__attribute__((noinline)) static void fill_stack(uint8_t v)
+{
+    volatile uint8_t junk[1 << 16];
+    for (size_t i = 0; i < sizeof(junk); ++i)
+        junk[i] = v;
+    asm volatile("" ::"r"(junk) : "memory");
+}
+
+// p4Enc256v64 is a loop of p4Enc128v64 over 128-value chunks
+// (p4enc256v64_scalar.cpp:15-30), so with `chunked` the 256v64 encoding is
+// made chunk by chunk with the stack refilled before each call (the direct
+// call's second chunk would see the first chunk's stale stack instead).
+static uint32_t enc64_ref(const std::vector<uint64_t> & in, unsigned n, bool d1, uint64_t start, bool v128, uint8_t fill,
+                          std::vector<uint8_t> & enc, bool chunked)
+{
+    std::vector<uint64_t> buf(in);
+    std::fill(enc.begin(), enc.end(), 0);
+    if (v128 || !chunked)
+    {
+        fill_stack(fill);
+        uint8_t * e = v128 ? (d1 ? sc::p4D1Enc128v64(buf.data(), n, enc.data(), start) : sc::p4Enc128v64(buf.data(), n, enc.data()))
+                           : (d1 ? sc::p4D1Enc256v64(buf.data(), n, enc.data(), start) : sc::p4Enc256v64(buf.data(), n, enc.data()));
+        return static_cast<uint32_t>(e - enc.data());
+    }
+    uint8_t * e = enc.data();
+    for (unsigned c0 = 0; c0 < n; c0 += 128u)
+    {
+        const unsigned c = std::min(n - c0, 128u);
+        fill_stack(fill);
+        e = d1 ? sc::p4D1Enc128v64(buf.data() + c0, c, e, c0 ? buf[c0 - 1] : start) : sc::p4Enc128v64(buf.data() + c0, c, e);
+    }
+    return static_cast<uint32_t>(e - enc.data());
+}
+
+static void add64_short(Writer & w, std::vector<uint64_t> v, bool d1, uint64_t start, bool v128)
+{
+    const unsigned n = static_cast<unsigned>(v.size());
+    std::vector<uint64_t> in(256 + 64, 0);
+    std::copy(v.begin(), v.end(), in.begin());
+    std::vector<uint8_t> e0(n * 10 + 4096), e1(n * 10 + 4096), ed(n * 10 + 4096);
+    const uint32_t len0 = enc64_ref(in, n, d1, start, v128, 0x00, e0, true);
+    const uint32_t len1 = enc64_ref(in, n, d1, start, v128, 0xA5, e1, true);
+    const uint32_t lend = enc64_ref(in, n, d1, start, v128, 0x00, ed, false);
+    if (len0 != len1 || len0 != lend)
+        die("64 short: length depends on stack contents", w.count);
+    const bool unpinned = std::memcmp(e0.data(), e1.data(), len0) != 0 || std::memcmp(e0.data(), ed.data(), len0) != 0;
+    std::vector<uint64_t> dec(256 + 64, 0);
+    const uint8_t * rp = v128 ? (d1 ? sc::p4D1Dec128v64(e0.data(), n, dec.data(), start) : sc::p4Dec128v64(e0.data(), n, dec.data()))
+                              : (d1 ? sc::p4D1Dec256v64(e0.data(), n, dec.data(), start) : sc::p4Dec256v64(e0.data(), n, dec.data()));
+    if (rp != e0.data() + len0)
+        die("64 short decode end pointer", w.count);
+    if (std::memcmp(dec.data(), v.data(), n * 8u) != 0)
+        die("64 short round trip", w.count);
+    w.record((d1 ? 1u : 0u) | (unpinned ? 4u : 0u), n, start, 8u, v.data(), e0.data(), len0);
+}
+
+static void gen64_short(Writer & w, uint64_t seed, bool v128)
+{
+    Rng r(seed);
+    const std::vector<unsigned> ns = v128 ? std::vector<unsigned>{1u, 7u, 64u, 100u, 127u}
+                                          : std::vector<unsigned>{1u, 100u, 128u, 129u, 200u, 255u};
+    for (unsigned n : ns)
+    {
+        std::vector<uint64_t> v(n);
+        std::fill(v.begin(), v.end(), 0ull);
+        add64_short(w, v, false, 0, v128);
+        std::fill(v.begin(), v.end(), 0x123456789ull);
+        add64_short(w, v, false, 0, v128); // constant
+        for (unsigned b : {8u, 40u})
+        {
+            for (auto & x : v)
+                x = r.range(0, (1ull << b) - 1ull);
+            add64_short(w, v, false, 0, v128); // plain (or patched by chance)
+        }
+        for (unsigned pct : {10u, 30u})
+            for (unsigned hi : {33u, 64u})
+            {
+                for (auto & x : v)
+                    x = (r.range(0, 99) < pct) ? r.range(1ull << (hi - 1), hi == 64 ? ~0ull : ((1ull << hi) - 1ull)) : r.range(0, 255);
+                add64_short(w, v, false, 0, v128); // bitmap or vbyte exceptions
+            }
+        for (auto & x : v)
+            x = r.range(0, 15);
+        v[r.range(0, n - 1)] = r.range(1u << 20, 1u << 30);
+        add64_short(w, v, false, 0, v128); // one exception: vbyte
+        for (uint64_t md : {1ull, 255ull, (1ull << 40)})
+        {
+            uint64_t cur = r.range(0, 100000), st = cur;
+            for (auto & x : v)
+                x = (cur += r.range(1, md));
+            add64_short(w, v, true, st, v128);
+        }
+    }
+}
+
 // Hand-made decode-only vectors: valid streams the encoder never emits.
 static void genDecodeOnly(Writer & w)
 {
@@ -393,11 +496,13 @@ int main(int argc, char ** argv)
     {
         Writer w;
         gen64(w, 0x256064, false);
+        gen64_short(w, 0x256065, false);
         w.save(dir + "/g256v64.bin");
     }
     {
         Writer w;
         gen64(w, 0x128064, true);
+        gen64_short(w, 0x128065, true);
         w.save(dir + "/g128v64.bin");
     }
     return 0;

@@ -17,6 +17,37 @@
 #include "turbopfor.h"           // /root/reference/include
 #include "scalar/p4_scalar.h"    // /root/reference/src
 
+namespace
+{
+template <class T, class Enc, class D1Enc>
+static uint64_t enc_batch(const T * in, uint64_t nb, const T * starts, uint8_t * out, uint64_t * off, Enc enc, D1Enc d1enc)
+{
+    T tmp[256 + 64];
+    uint8_t * p = out;
+    for (uint64_t i = 0; i < nb; ++i)
+    {
+        off[i] = static_cast<uint64_t>(p - out);
+        std::memcpy(tmp, in + i * 256u, 256u * sizeof(T));
+        p = starts ? d1enc(tmp, 256u, p, starts[i]) : enc(tmp, 256u, p);
+    }
+    off[nb] = static_cast<uint64_t>(p - out);
+    return off[nb];
+}
+
+template <class T, class Dec, class D1Dec>
+static int64_t dec_batch(const uint8_t * in, const uint64_t * off, uint64_t nb, const T * starts, T * out, Dec dec, D1Dec d1dec)
+{
+    for (uint64_t i = 0; i < nb; ++i)
+    {
+        const uint8_t * e = starts ? d1dec(in + off[i], 256u, out + i * 256u, starts[i]) : dec(in + off[i], 256u, out + i * 256u);
+        if (e != in + off[i + 1])
+            return static_cast<int64_t>(i);
+    }
+    return -1;
+}
+
+} // namespace
+
 extern "C" {
 
 #define W32ENC(name, ns, fn) \
@@ -60,6 +91,32 @@ extern "C" {
 
 FAMILY(tpref_s_, turbopfor::scalar)
 FAMILY(tpref_d_, turbopfor)
+
+// Batch round trips through the reference SCALAR path (the parity oracle),
+// for tests that pin the C restatement on the bench distributions: block i
+// is in[256i..] (D1 when starts != nullptr, starts[i] = the value before the
+// block); encodings end to end with off[i] the byte offset of block i.
+// Decode returns -1 when every block ends exactly at off[i+1], else the
+// first block that does not.
+uint64_t tpref_s_enc256v32_batch(const uint32_t * in, uint64_t nb, const uint32_t * starts, uint8_t * out, uint64_t * off)
+{
+    return enc_batch<uint32_t>(in, nb, starts, out, off, turbopfor::scalar::p4Enc256v32, turbopfor::scalar::p4D1Enc256v32);
+}
+
+int64_t tpref_s_dec256v32_batch(const uint8_t * in, const uint64_t * off, uint64_t nb, const uint32_t * starts, uint32_t * out)
+{
+    return dec_batch<uint32_t>(in, off, nb, starts, out, turbopfor::scalar::p4Dec256v32, turbopfor::scalar::p4D1Dec256v32);
+}
+
+uint64_t tpref_s_enc256v64_batch(const uint64_t * in, uint64_t nb, const uint64_t * starts, uint8_t * out, uint64_t * off)
+{
+    return enc_batch<uint64_t>(in, nb, starts, out, off, turbopfor::scalar::p4Enc256v64, turbopfor::scalar::p4D1Enc256v64);
+}
+
+int64_t tpref_s_dec256v64_batch(const uint8_t * in, const uint64_t * off, uint64_t nb, const uint64_t * starts, uint64_t * out)
+{
+    return dec_batch<uint64_t>(in, off, nb, starts, out, turbopfor::scalar::p4Dec256v64, turbopfor::scalar::p4D1Dec256v64);
+}
 
 // Streaming decode of nblocks consecutive 256v32 blocks (block i at
 // in+off[i]) on nthreads std::threads, each a contiguous block range.

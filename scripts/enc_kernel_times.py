@@ -1,6 +1,7 @@
 """Encoder kernel timing (measurement tool; run under rocprofv3 --kernel-trace
 --stats for per-kernel times): C4-mix 256v32 encode, `reps` launches.
-usage: python scripts/enc_kernel_times.py [nblocks] [reps]"""
+usage: python scripts/enc_kernel_times.py [nblocks] [reps] [probe]
+probe 1/2: tpf_probe_enc256v32 (the plan / write pass with the coding removed)"""
 import os
 import sys
 
@@ -14,11 +15,15 @@ import bench  # noqa: E402
 
 nb = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+probe = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 dev = torch.device("cuda:0")
 vals, _ = bench.gen_c2(nb, 0, seed=11, dev=dev, pcts=[0, 5, 10, 25])
 cap = int(tpf.lib().tpf_p4enc256v32_bound(nb))
 out = torch.empty(cap, dtype=torch.uint8, device=dev)
 for _ in range(reps):
-    tpf.enc256v32(vals, out=out)
+    if probe:
+        tpf.probe_enc256v32(probe, vals, out)
+    else:
+        tpf.enc256v32(vals, out=out)
 torch.cuda.synchronize()
-print("done", os.environ.get("TPF_ENC_PROBE", "0"))
+print("done", probe)

@@ -4,8 +4,13 @@ bench.py reports as roofline.traffic.  Per MI355X_MICROARCH.md §HBM:
 FETCH_SIZE counts half the bytes of 16 B/lane streaming reads on gfx950
 (double it), WRITE_SIZE is exact for 16 B/lane stores; both are in KiB.
 
-usage: python scripts/pmc_traffic.py WORKLOAD FETCH_CSV WRITE_CSV NBLOCKS OUT_JSON"""
+Each entry records the md5 of the library the counters were taken with
+(lib_md5) and a label: bench.py replays the number only while it runs that
+same library, and says so (roofline.traffic_source).
+
+usage: python scripts/pmc_traffic.py WORKLOAD FETCH_CSV WRITE_CSV NBLOCKS OUT_JSON [LABEL]"""
 import csv
+import hashlib
 import json
 import os
 import statistics
@@ -41,8 +46,20 @@ def per_launch(path, counter, test):
     return statistics.median(vals), len(vals)
 
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "turbopfor-cpp_amd", "lib", "libturbopfor_amd.so")
+
+
+def lib_md5(path=LIB):
+    try:
+        return hashlib.md5(open(path, "rb").read()).hexdigest()
+    except OSError:
+        return None
+
+
 def main():
     wl, fetch_csv, write_csv, nblocks, out = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5]
+    label = sys.argv[6] if len(sys.argv) > 6 else None
     tests, kname = KERNELS[wl]
     f_kib = w_kib = 0.0
     nf, nw = [], []
@@ -55,7 +72,7 @@ def main():
     hbm = (2.0 * f_kib + w_kib) * 1024.0
     d = {"workload": wl, "nblocks": nblocks, "kernel": kname,
          "FETCH_SIZE_KiB_median": f_kib, "WRITE_SIZE_KiB_median": w_kib, "launches": [nf, nw],
-         "hbm_bytes_per_launch": int(hbm),
+         "hbm_bytes_per_launch": int(hbm), "label": label, "lib_md5": lib_md5(),
          "correction": "hbm = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (gfx950 FETCH_SIZE halves 16B/lane reads)"}
     allv = {}
     if os.path.exists(out):

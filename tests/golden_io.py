@@ -9,11 +9,15 @@ GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 class Record:
-    __slots__ = ("d1", "decode_only", "n", "start", "esize", "values", "enc")
+    __slots__ = ("d1", "decode_only", "padding_unpinned", "n", "start", "esize", "values", "enc")
 
     def __init__(self, flags, n, start, esize, values, enc):
         self.d1 = bool(flags & 1)
         self.decode_only = bool(flags & 2)
+        # flag 4: n below the layout width and the reference's bytes for the
+        # padding slots depend on its uninitialised stack (oracle/gen_golden.cpp
+        # gen64_short): compare the length and the decoded values, not the bytes
+        self.padding_unpinned = bool(flags & 4)
         self.n = n
         self.start = start
         self.esize = esize

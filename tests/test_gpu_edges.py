@@ -103,3 +103,80 @@ def test_hipgraph_capture_replay():
         torch.cuda.synchronize()
         assert torch.equal(out, vals)
         assert int(err.item()) == -1
+
+
+def _host_abi():
+    L = tpf.lib()
+    L.tpf_host_dec.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                               ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]
+    return L
+
+
+def test_host_dec_rejects_bad_offsets_and_reports_corrupt_block():
+    """tpf_host_dec with caller offsets: decreasing or past in_bytes -> TPF_EINVAL
+    before any copy; a block whose parsed length disagrees with its offsets ->
+    TPF_ECORRUPT naming the block (offsets were trusted)."""
+    import oracle_lib
+
+    rng = np.random.default_rng(5)
+    nb = 3000
+    vals = rng.integers(0, 1 << 12, size=(nb, 256), dtype=np.uint64).astype(np.uint32)
+    packed, off = oracle_lib.enc256v32_batch(vals)
+    L = _host_abi()
+    out = np.zeros((nb, 256), dtype=np.uint32)
+
+    def run(o, nbytes=len(packed)):
+        o = np.ascontiguousarray(o, dtype=np.uint64)
+        return L.tpf_host_dec(2, packed.ctypes.data, nbytes, o.ctypes.data, nb, 256, out.ctypes.data, None)
+
+    assert run(off) == 0
+    np.testing.assert_array_equal(out, vals)
+    bad = off.copy()
+    bad[10], bad[11] = bad[11], bad[10]  # a descending pair
+    assert run(bad) == -1 and b"decreases" in L.tpf_last_error()
+    assert run(off, nbytes=len(packed) - 1) == -1 and b"in_bytes" in L.tpf_last_error()
+    bad = off.copy()
+    bad[1234] += 1  # block 1233 one byte too long, 1234 one too short
+    assert run(bad) == -4
+    assert b"block 1233" in L.tpf_last_error()
+
+
+def test_encoder_rejects_small_out_cap():
+    """The encoded sizes are only known on the device: a capacity below the
+    bound is rejected up front rather than cutting blocks off silently."""
+    L = tpf.lib()
+    nb = 64
+    vals = torch.zeros((nb, 256), dtype=torch.int32, device=DEV)
+    cap = int(L.tpf_p4enc256v32_bound(nb))
+    out = torch.empty(cap, dtype=torch.uint8, device=DEV)
+    offs = torch.empty(nb + 1, dtype=torch.int64, device=DEV)
+    wsb = int(L.tpf_p4enc256v32_workspace_size(nb))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=DEV)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert L.tpf_p4enc256v32_batch(vals.data_ptr(), nb, out.data_ptr(), cap - 1, offs.data_ptr(), ws.data_ptr(), wsb, s) == -1
+    assert b"out_cap" in L.tpf_last_error()
+    assert L.tpf_p4enc256v32_batch(vals.data_ptr(), nb, out.data_ptr(), cap, offs.data_ptr(), ws.data_ptr(), wsb, s) == 0
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("fmt,n", [("128v32", 100), ("256v32", 200), ("128v64", 100)])
+def test_chained_d1_encode_with_short_units(fmt, n):
+    """One chained list over units of n < width values: unit i starts from
+    unit i-1's value n-1 (the slots after it are padding), as a reference
+    caller chaining p4D1Enc<fmt>(in + i*width, n, out, in[i*width + n - 1])."""
+    import oracle_lib
+
+    wide = fmt == "128v64"
+    dt = np.uint64 if wide else np.uint32
+    width = tpf.unit_values(fmt, n)
+    nb = 200
+    rng = np.random.default_rng(n)
+    lst = np.cumsum(rng.integers(1, 300, size=nb * n)).astype(dt).reshape(nb, n)
+    vals = np.zeros((nb, width), dtype=dt)
+    vals[:, :n] = lst
+    vals[:, n:] = 0xDEAD  # padding must not feed the next unit's start
+    start0 = 17
+    exp = b"".join(oracle_lib.encode(fmt, lst[i], d1=True, start=int(lst[i - 1, -1]) if i else start0) for i in range(nb))
+    t = torch.from_numpy(vals.view(np.int64 if wide else np.int32).ravel()).to(DEV)
+    packed, offs = tpf.enc_batch(fmt, t, nb, n, d1=True, start0=start0)
+    assert packed.cpu().numpy().tobytes() == exp

@@ -27,9 +27,13 @@ def to_dev(arr, wide):
     return torch.from_numpy(a.view(np.int64 if wide else np.int32)).to(DEV)
 
 
-def groups(fname):
+def groups(fname, fmt):
+    """Golden records by (n, d1).  Batches hold whole 256v64 units; shorter
+    256v64 vectors go through the per-block API (test_gpu_dropin.py)."""
     g = collections.defaultdict(list)
     for r in golden_io.load(fname):
+        if fmt == "256v64" and r.n != 256:
+            continue
         g[(r.n, r.d1)].append(r)
     return g
 
@@ -37,7 +41,7 @@ def groups(fname):
 @pytest.mark.parametrize("fname,fmt", FAMILIES)
 def test_golden_encode(fname, fmt):
     wide = fmt in ("64", "128v64", "256v64")
-    for (n, d1), recs in groups(fname).items():
+    for (n, d1), recs in groups(fname, fmt).items():
         recs = [r for r in recs if not r.decode_only]
         if not recs:
             continue
@@ -50,13 +54,18 @@ def test_golden_encode(fname, fmt):
         pk = packed.cpu().numpy().tobytes()
         of = offs.cpu().numpy()
         for i, r in enumerate(recs):
-            assert pk[of[i]:of[i + 1]] == r.enc, f"{fmt} n={n} d1={d1} record {i}"
+            mine = pk[of[i]:of[i + 1]]
+            if r.padding_unpinned:  # padding bits: the zero convention (oracle), length as the reference
+                assert len(mine) == len(r.enc), f"{fmt} n={n} d1={d1} record {i}"
+                assert mine == oracle_lib.encode(fmt, r.values, d1=d1, start=r.start), f"{fmt} n={n} record {i}"
+            else:
+                assert mine == r.enc, f"{fmt} n={n} d1={d1} record {i}"
 
 
 @pytest.mark.parametrize("fname,fmt", FAMILIES)
 def test_golden_decode(fname, fmt):
     wide = fmt in ("64", "128v64", "256v64")
-    for (n, d1), recs in groups(fname).items():
+    for (n, d1), recs in groups(fname, fmt).items():
         u = tpf.unit_values(fmt, n)
         offs = np.zeros(len(recs) + 1, dtype=np.int64)
         offs[1:] = np.cumsum([len(r.enc) for r in recs])

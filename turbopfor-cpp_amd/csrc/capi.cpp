@@ -107,6 +107,16 @@ int tpf_probe256v32(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_
     return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_probe256v32");
 }
 
+int tpf_probe_hbm(int kind, void * d_dst, const void * d_src, uint64_t bytes, void * stream)
+{
+    if (int rc = check_device())
+        return rc;
+    if (kind < 0 || kind > 2 || !d_dst || (kind != 1 && !d_src))
+        return fail(TPF_EINVAL, "tpf_probe_hbm: bad kind or null pointer");
+    hipError_t e = tpf::launch_probe_hbm(kind, d_dst, d_src, bytes, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_probe_hbm");
+}
+
 int tpf_p4d1dec256v32_batch(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nblocks, uint32_t * d_out,
                             const uint32_t * d_starts, uint64_t * d_err, void * stream)
 {
@@ -188,6 +198,10 @@ static int enc256v32_common(const uint32_t * d_in, uint64_t nblocks, const uint3
         return fail(TPF_EINVAL, std::string(name) + ": null pointer");
     if (ws_bytes < tpf::enc256v32_workspace(nblocks))
         return fail(TPF_EINVAL, std::string(name) + ": workspace too small");
+    // the encoded sizes are known only on the device: the caller's capacity
+    // must cover the worst case, or a block could be cut off unreported
+    if (nblocks && out_cap < tpf_p4enc256v32_bound(nblocks))
+        return fail(TPF_EINVAL, std::string(name) + ": out_cap below tpf_p4enc256v32_bound(nblocks)");
     hipError_t e = tpf::launch_enc256v32(d_in, nblocks, d_starts, start0, d1, d_out, out_cap, d_off, d_ws, ws_bytes,
                                          static_cast<hipStream_t>(stream));
     return e == hipSuccess ? TPF_OK : hip_fail(e, name);
@@ -197,6 +211,20 @@ int tpf_p4enc256v32_batch(const uint32_t * d_in, uint64_t nblocks, uint8_t * d_o
                           size_t ws_bytes, void * stream)
 {
     return enc256v32_common(d_in, nblocks, nullptr, 0, false, d_out, out_cap, d_off, d_ws, ws_bytes, stream, "tpf_p4enc256v32_batch");
+}
+
+int tpf_probe_enc256v32(int mode, const uint32_t * d_in, uint64_t nblocks, uint8_t * d_out, uint64_t out_cap, uint64_t * d_off,
+                        void * d_ws, size_t ws_bytes, void * stream)
+{
+    if (int rc = check_device())
+        return rc;
+    if (mode < 1 || mode > 2 || !d_off || (nblocks && (!d_in || !d_out || !d_ws)))
+        return fail(TPF_EINVAL, "tpf_probe_enc256v32: bad mode or null pointer");
+    if (ws_bytes < tpf::enc256v32_workspace(nblocks))
+        return fail(TPF_EINVAL, "tpf_probe_enc256v32: workspace too small");
+    hipError_t e = tpf::launch_enc256v32(d_in, nblocks, nullptr, 0, false, d_out, out_cap, d_off, d_ws, ws_bytes,
+                                         static_cast<hipStream_t>(stream), mode);
+    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_probe_enc256v32");
 }
 
 int tpf_p4d1enc256v32_batch(const uint32_t * d_in, uint64_t nblocks, const uint32_t * d_starts, uint32_t start0, uint8_t * d_out,
@@ -217,9 +245,9 @@ static bool fmt_ok(int fmt, unsigned n)
             return n >= 1 && n <= 128;
         case TPF_FMT_256V32:
             return n >= 1 && n <= 256;
-        case TPF_FMT_128V64:
-            return n == 128;
-        case TPF_FMT_256V64:
+        case TPF_FMT_128V64: // n < 128: bitmap of pad8(n), exceptions over n values, full-width base
+            return n >= 1 && n <= 128;
+        case TPF_FMT_256V64: // batches of 256v64 units hold full units (the per-block API splits n < 256)
             return n == 256;
         default:
             return false;
@@ -289,6 +317,8 @@ int tpf_enc_batch(int fmt, const void * d_vals, uint64_t nblocks, unsigned n, in
         return fail(TPF_EINVAL, "tpf_enc_batch: null pointer");
     if (ws_bytes < tpf_enc_workspace_size(fmt, nblocks, n))
         return fail(TPF_EINVAL, "tpf_enc_batch: workspace too small");
+    if (nblocks && out_cap < tpf_enc_bound(fmt, nblocks, n))
+        return fail(TPF_EINVAL, "tpf_enc_batch: out_cap below tpf_enc_bound(fmt, nblocks, n)");
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipError_t e;
     if (fmt == TPF_FMT_256V32 && n == 256)

@@ -125,15 +125,18 @@ uint64_t tpf_block_size(int fmt, const uint8_t * in, uint64_t avail, unsigned n,
         return 0;
     if (fmt == TPF_FMT_256V64)
     {
+        // consecutive 128v64 blocks of min(remaining, 128) values (p4dec256v64_scalar.cpp:37-51);
+        // a non-constant block writes all 128 slots, a constant one its n values
+        const unsigned n0 = n < 128u ? n : 128u;
         int c1 = 0;
-        const uint64_t a = one_block(TPF_FMT_128V64, in, avail, 128, &cst);
+        const uint64_t a = one_block(TPF_FMT_128V64, in, avail, n0, &cst);
         if (!a)
             return 0;
-        const uint64_t b = one_block(TPF_FMT_128V64, in + a, avail - a, 128, &c1);
-        if (!b)
+        uint64_t b = 0;
+        if (n > 128u && !(b = one_block(TPF_FMT_128V64, in + a, avail - a, n - 128u, &c1)))
             return 0;
         if (values_written)
-            *values_written = 256;
+            *values_written = n > 128u ? static_cast<int>(128u + (c1 ? n - 128u : 128u)) : static_cast<int>(cst ? n : 128u);
         return a + b;
     }
     const uint64_t sz = one_block(fmt, in, avail, n, &cst);

@@ -305,18 +305,37 @@ const unsigned char * p4D1Dec128v64(const unsigned char * in, unsigned n, uint64
     return dec_one(TPF_FMT_128V64, in, n, out, true, start);
 }
 
-unsigned char * p4Enc256v64(uint64_t * in, unsigned n, unsigned char * out) { return enc_one(TPF_FMT_256V64, in, n, out, false, 0); }
+// 256v64 = consecutive 128v64 blocks of min(remaining, 128) values
+// (p4enc256v64_scalar.cpp:15-30, p4d1dec256v64_scalar.cpp:15-49): a full
+// 256-value unit goes to the paired kernels in one launch, a shorter one as
+// its 128v64 blocks (the second starting from value 127 for D1).
+unsigned char * p4Enc256v64(uint64_t * in, unsigned n, unsigned char * out)
+{
+    if (n == 256u || n == 0u)
+        return enc_one(TPF_FMT_256V64, in, n, out, false, 0);
+    out = enc_one(TPF_FMT_128V64, in, std::min(n, 128u), out, false, 0);
+    return n > 128u ? enc_one(TPF_FMT_128V64, in + 128, n - 128u, out, false, 0) : out;
+}
 unsigned char * p4D1Enc256v64(uint64_t * in, unsigned n, unsigned char * out, uint64_t start)
 {
-    return enc_one(TPF_FMT_256V64, in, n, out, true, start);
+    if (n == 256u || n == 0u)
+        return enc_one(TPF_FMT_256V64, in, n, out, true, start);
+    out = enc_one(TPF_FMT_128V64, in, std::min(n, 128u), out, true, start);
+    return n > 128u ? enc_one(TPF_FMT_128V64, in + 128, n - 128u, out, true, in[127]) : out;
 }
 const unsigned char * p4Dec256v64(const unsigned char * in, unsigned n, uint64_t * out)
 {
-    return dec_one(TPF_FMT_256V64, in, n, out, false, 0);
+    if (n == 256u || n == 0u)
+        return dec_one(TPF_FMT_256V64, in, n, out, false, 0);
+    in = dec_one(TPF_FMT_128V64, in, std::min(n, 128u), out, false, 0);
+    return n > 128u ? dec_one(TPF_FMT_128V64, in, n - 128u, out + 128, false, 0) : in;
 }
 const unsigned char * p4D1Dec256v64(const unsigned char * in, unsigned n, uint64_t * out, uint64_t start)
 {
-    return dec_one(TPF_FMT_256V64, in, n, out, true, start);
+    if (n == 256u || n == 0u)
+        return dec_one(TPF_FMT_256V64, in, n, out, true, start);
+    in = dec_one(TPF_FMT_128V64, in, std::min(n, 128u), out, true, start);
+    return n > 128u ? dec_one(TPF_FMT_128V64, in, n - 128u, out + 128, true, out[127]) : in;
 }
 } // namespace turbopfor
 

@@ -167,6 +167,8 @@ struct Slot
 {
     hipEvent_t up = nullptr, mid = nullptr, done = nullptr;
     Buf in, vals, ws, start, off, hoff{true};
+    Buf derr, herr{true}; // decode: the chunk's first inconsistent block (device word, pinned copy)
+    uint64_t c0 = ~0ull;  // decode: first block of the chunk the slot last carried (~0: none)
     Slot()
     {
         for (hipEvent_t * e : {&up, &mid, &done})
@@ -278,6 +280,15 @@ int tpf_host_dec(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_
                 throw Err(TPF_ECORRUPT, "tpf_host_dec: malformed block while scanning offsets");
             h_off = scanned.data();
         }
+        else
+        {
+            // caller-supplied offsets bound every upload: they must rise and stay inside h_in
+            for (uint64_t i = 0; i < nblocks; ++i)
+                if (h_off[i] > h_off[i + 1])
+                    throw Err(TPF_EINVAL, "tpf_host_dec: h_off decreases at block " + std::to_string(i));
+            if (h_off[nblocks] > in_bytes)
+                throw Err(TPF_EINVAL, "tpf_host_dec: h_off[nblocks] is past in_bytes");
+        }
         const size_t es = wide_fmt(fmt) ? 8 : 4;
         const size_t uv = unit_values(fmt, n);
         const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(nblocks, chunk_value_bytes() / (es * uv)));
@@ -291,11 +302,24 @@ int tpf_host_dec(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_
         }
         Lease lease;
         Pipeline & P = *lease.p;
+        uint64_t bad = ~0ull; // first block whose parsed length disagrees with its offsets
+        auto collect = [&](Slot & sl) {
+            if (sl.c0 != ~0ull)
+            {
+                const uint64_t e = *static_cast<const uint64_t *>(sl.herr.p);
+                if (e != ~0ull)
+                    bad = std::min(bad, sl.c0 + e);
+            }
+            sl.c0 = ~0ull;
+        };
+        for (Slot & sl : P.slots)
+            sl.c0 = ~0ull;
         uint64_t k = 0;
         for (uint64_t c0 = 0; c0 < nblocks; c0 += chunk, ++k)
         {
             Slot & sl = P.slots[k % kSlots];
             hc(hipEventSynchronize(sl.done), "wait slot"); // chunk k-kSlots is done with the slot
+            collect(sl);
             const uint64_t c1 = std::min(nblocks, c0 + chunk);
             const uint64_t nb = c1 - c0;
             const uint64_t b0 = h_off[c0], bytes = h_off[c1] - b0;
@@ -313,7 +337,11 @@ int tpf_host_dec(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_
                    "H2D starts");
             hc(hipEventRecord(sl.up, P.cs), "record up");
             hc(hipStreamWaitEvent(P.ks, sl.up, 0), "wait up");
-            tc(tpf_dec_batch(fmt, d_in, bytes, d_off, nb, n, out, d_start, nullptr, P.ks));
+            auto * d_err = static_cast<uint64_t *>(sl.derr.get(8));
+            sl.herr.get(8);
+            tc(tpf_dec_batch(fmt, d_in, bytes, d_off, nb, n, out, d_start, d_err, P.ks));
+            hc(hipMemcpyAsync(sl.herr.p, d_err, 8, hipMemcpyDeviceToHost, P.ks), "D2H err");
+            sl.c0 = c0;
             if (!dv)
                 hc(hipMemcpyAsync(static_cast<uint8_t *>(h_vals) + c0 * uv * es, out, nb * uv * es, hipMemcpyDeviceToHost, P.ks),
                    "D2H vals");
@@ -321,6 +349,10 @@ int tpf_host_dec(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_
         }
         hc(hipStreamSynchronize(P.ks), "sync");
         lease.ok = true;
+        for (Slot & sl : P.slots)
+            collect(sl);
+        if (bad != ~0ull)
+            throw Err(TPF_ECORRUPT, "tpf_host_dec: block " + std::to_string(bad) + " parses to a length other than its offsets");
         return TPF_OK;
     }
     catch (const Err & e)
@@ -402,8 +434,9 @@ int tpf_host_enc(int fmt, const void * h_vals, uint64_t nblocks, unsigned n, int
             }
             else if (d1 && c0 > 0)
             {
-                // chained list: this chunk starts after the previous chunk's last input value
-                const uint8_t * last = static_cast<const uint8_t *>(h_vals) + (c0 * uv - 1) * es;
+                // chained list: this chunk starts after the previous chunk's last
+                // input value (the previous unit's value n-1: slots past n are padding)
+                const uint8_t * last = static_cast<const uint8_t *>(h_vals) + ((c0 - 1) * uv + n - 1) * es;
                 s0 = 0;
                 std::memcpy(&s0, last, es);
             }

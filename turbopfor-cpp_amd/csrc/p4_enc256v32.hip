@@ -15,14 +15,13 @@
 // the next two blocks in flight (the first version loaded one block per loop
 // iteration and waited for it: 5.0 and 5.4 ms per 10M blocks, latency-bound).
 //
-// TPF_ENC_PROBE (measurement only -- the output is NOT a valid stream): 1 =
+// probe != 0 (measurement only, reachable only through the separate
+// tpf_probe_enc256v32 entry point -- the output is NOT a valid stream): 1 =
 // plan kernel with the cost model replaced by a wave OR, 2 = write kernel
 // copying the staged values instead of building blocks; same loads and
 // stores, so they time each pass's data-movement ceiling
 // (scripts/gpu_enc_probe.sh, profiles/r1_v4_enc_probe.txt).
 #include <hipcub/hipcub.hpp>
-
-#include <cstdlib>
 
 #include "p4_enc32.h"
 #include "tpf_kernels.h"
@@ -229,7 +228,8 @@ size_t enc256v32_workspace(uint64_t nblocks)
 }
 
 hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, bool d1,
-                            uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t stream)
+                            uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t stream,
+                            int probe)
 {
     if (nblocks == 0)
         return hipMemsetAsync(off, 0, sizeof(uint64_t), stream);
@@ -241,8 +241,6 @@ hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_
     size_t scan_bytes = ws_bytes > plan_bytes ? ws_bytes - plan_bytes : 0;
     const uint64_t per_wg = 4ull * dev::kEncRun;
     const uint32_t grid = static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg);
-    const char * pe = std::getenv("TPF_ENC_PROBE");
-    const int probe = pe ? std::atoi(pe) : 0;
     if (d1)
         hipLaunchKernelGGL(dev::k_enc256v32_plan<true>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan);
     else if (probe == 1)

@@ -122,11 +122,12 @@ struct EncRunG
 {
     using T = typename FmtTraits<F>::T;
     uint64_t first;
-    uint32_t nr, pu, NE;
+    uint32_t nr, pu, NE, n;
     __amdgpu_buffer_rsrc_t rs;
 
-    __device__ __forceinline__ bool init(const T * in, uint64_t nblocks, uint32_t wv, uint32_t n)
+    __device__ __forceinline__ bool init(const T * in, uint64_t nblocks, uint32_t wv, uint32_t n_values)
     {
+        n = n_values;
         first = (static_cast<uint64_t>(blockIdx.x) * 4u + wv) * kGRun;
         if (first >= nblocks)
             return false;
@@ -164,7 +165,9 @@ struct EncRunG
         const uint64_t blk = first + t;
         if (starts)
             return starts[blk];
-        return blk == 0 ? start0 : in[blk * pu - 1u];
+        // the previous unit's last real value: with n below the layout's
+        // width (128v32/256v32/128v64 units) the slots after it are padding
+        return blk == 0 ? start0 : in[(blk - 1u) * pu + n - 1u];
     }
 };
 
@@ -400,7 +403,9 @@ hipError_t launch_dec_generic(int fmt, const uint8_t * in, uint64_t in_bytes, co
             return dec_fmt<dev::Fmt::V256>(in, in_bytes, off, nblocks, n, out, starts, err, s);
         case FMT_64:
             return dec_fmt<dev::Fmt::H64>(in, in_bytes, off, nblocks, n, out, starts, err, s);
-        case FMT_128V64: // run-pipelined kernel, p4_dec256v64.hip
+        case FMT_128V64: // run-pipelined kernel, p4_dec256v64.hip (n < 128: the generic one)
+            if (n < 128u)
+                return dec_fmt<dev::Fmt::V128X64>(in, in_bytes, off, nblocks, n, out, starts, err, s);
             return launch_dec128v64(1, in, in_bytes, off, nblocks, static_cast<uint64_t *>(out),
                                     static_cast<const uint64_t *>(starts), err, s);
         case FMT_256V64:
@@ -428,7 +433,10 @@ hipError_t launch_enc_generic(int fmt, const void * in, uint64_t nblocks, uint32
             return enc_fmt<dev::Fmt::V256>(in, nblocks, n, d1, starts, start0, out, out_cap, off, ws, ws_bytes, s);
         case FMT_64:
             return enc_fmt<dev::Fmt::H64>(in, nblocks, n, d1, starts, start0, out, out_cap, off, ws, ws_bytes, s);
-        case FMT_128V64: // run-pipelined kernels, p4_enc256v64.hip
+        case FMT_128V64: // run-pipelined kernels, p4_enc256v64.hip (n < 128: the generic ones)
+            if (n < 128u)
+                return enc_fmt<dev::Fmt::V128X64>(in, nblocks, n, d1, starts, start0, out, out_cap, off, ws, ws_bytes, s);
+            [[fallthrough]];
         case FMT_256V64:
             return launch_enc128v64(fmt == FMT_256V64 ? 2u : 1u, static_cast<const uint64_t *>(in), nblocks, d1,
                                     static_cast<const uint64_t *>(starts), start0, out, out_cap, off, ws, ws_bytes, s);

@@ -32,6 +32,8 @@ hipError_t launch_copy(void * dst, const void * src, uint64_t bytes, hipStream_t
 hipError_t launch_append(uint8_t * dst, const uint8_t * src, const uint64_t * pos, const uint64_t * len, uint64_t * pos_out,
                          hipStream_t s);
 hipError_t launch_err_merge(unsigned long long * err, const unsigned long long * sub_err, uint64_t base, hipStream_t s);
+// Measurement only: streaming read / write / copy ceilings (hbm_probe.hip).
+hipError_t launch_probe_hbm(int kind, void * dst, const void * src, uint64_t bytes, hipStream_t s);
 
 size_t generic_workspace(uint64_t nblocks);
 hipError_t launch_dec_generic(int fmt, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t n,
@@ -60,6 +62,7 @@ hipError_t launch_enc128v64(uint32_t nb, const uint64_t * in, uint64_t nunits, b
 
 size_t enc256v32_workspace(uint64_t nblocks);
 hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, bool d1,
-                            uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t stream);
+                            uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t stream,
+                            int probe = 0);
 
 } // namespace tpf

@@ -47,6 +47,14 @@ def max_over_ranks(x, device, group=None):
     return float(t.item())
 
 
+def gather_floats(values, device, group=None):
+    """Every rank's list of floats (same length on every rank), rank order."""
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(out, t, group=group)
+    return [[float(v) for v in o.cpu().tolist()] for o in out]
+
+
 def all_ok(ok, device, group=None):
     t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)

@@ -47,6 +47,8 @@ def lib():
         L.tpf_p4dec256v32_batch.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp, c_vp]
         L.tpf_p4d1dec256v32_batch.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp, c_vp, c_vp]
         L.tpf_probe256v32.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp]
+        L.tpf_probe_hbm.argtypes = [ctypes.c_int, c_vp, c_vp, c_u64, c_vp]
+        L.tpf_probe_enc256v32.argtypes = [ctypes.c_int, c_vp, c_u64, c_vp, c_u64, c_vp, c_vp, ctypes.c_size_t, c_vp]
         L.tpf_p4enc256v32_bound.argtypes = [c_u64]
         L.tpf_p4enc256v32_bound.restype = c_u64
         L.tpf_p4enc256v32_workspace_size.argtypes = [c_u64]
@@ -79,7 +81,8 @@ def lib():
                                        ctypes.c_size_t, c_vp, c_vp]
         for name in ("tpf_p4nenc256v32", "tpf_p4ndec256v32", "tpf_p4dec256v32_batch", "tpf_p4d1dec256v32_batch", "tpf_p4enc256v32_batch",
                      "tpf_p4d1enc256v32_batch", "tpf_dec_batch", "tpf_enc_batch", "tpf_p4d1dec256v32_chained",
-                     "tpf_p4d1dec256v32_chain_sums", "tpf_p4d1dec256v32_chain_decode", "tpf_probe256v32"):
+                     "tpf_p4d1dec256v32_chain_sums", "tpf_p4d1dec256v32_chain_decode", "tpf_probe256v32",
+                     "tpf_probe_hbm", "tpf_probe_enc256v32"):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -125,6 +128,30 @@ def probe256v32(packed, offsets, nblocks, out):
 
     _check(lib().tpf_probe256v32(_ptr(packed), packed.numel(), _ptr(offsets), nblocks, _ptr(out), _stream(torch)))
     return out
+
+
+def probe_hbm(kind, dst, src, nbytes):
+    """Measurement only: streaming ceiling kernels (tpf_probe_hbm): kind
+    "read" (src), "write" (dst) or "copy" (src -> dst) of nbytes bytes."""
+    import torch
+
+    k = {"read": 0, "write": 1, "copy": 2}[kind]
+    _check(lib().tpf_probe_hbm(k, _ptr(dst), _ptr(src), nbytes, _stream(torch)))
+
+
+def probe_enc256v32(mode, values, out):
+    """Measurement only: the 256v32 encoder's passes with the coding removed
+    (mode 1 = plan pass as a wave OR, 2 = write pass copying values); the
+    output is not a valid stream."""
+    import torch
+
+    nb = values.numel() // 256
+    L = lib()
+    offs = torch.empty(nb + 1, dtype=torch.int64, device=values.device)
+    ws_bytes = int(L.tpf_p4enc256v32_workspace_size(nb))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=values.device)
+    _check(L.tpf_probe_enc256v32(mode, _ptr(values), nb, _ptr(out), out.numel(), _ptr(offs), _ptr(ws), ws_bytes,
+                                 _stream(torch)))
 
 
 def enc256v32(values, d1=False, starts=None, start0=0, out=None):
