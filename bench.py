@@ -490,7 +490,7 @@ class Timer:
 def per_rank_stats(world, dev, kernel_ms, achieved_GBps):
     """Every rank's average kernel time and HBM fraction (all_gather; rank 0 reports them)."""
     mine = [float(kernel_ms), float(achieved_GBps)]
-    rows = tpf_shard.gather_floats(mine, dev) if world > 1 else [mine]
+    rows = tpf_shard.gather_floats(mine, dev) if torch.distributed.is_initialized() else [mine]
     return [{"rank": r, "kernel_ms_avg": round(ms, 4), "achieved_GBps": round(gbs, 1),
              "frac": round(gbs / HBM_PEAK_GBS, 4)} for r, (ms, gbs) in enumerate(rows)]
 
@@ -533,7 +533,7 @@ def run_c2(args, world, rank, dev, T):
     elapsed, kern_ms = T.run(lambda: tpf.dec256v32(packed, offs, nb, out=out), args.steps, args.warmup)
     tpf.dec256v32(packed, offs, nb, out=out, err=err)
     ok = bool(torch.equal(out, vals)) and int(err.item()) == -1
-    if world > 1:
+    if T.dist_on:
         ok = tpf_shard.all_ok(ok, dev)
 
     e2e = None
@@ -615,7 +615,7 @@ def run_sweep(args, world, rank, dev, T):
                 + ("" if good else " MISMATCH"))
         del vals, packed, offs
     elapsed = time.perf_counter() - t_start
-    if world > 1:
+    if T.dist_on:
         ok = tpf_shard.all_ok(ok, dev)
     if rank != 0:
         return None
@@ -703,7 +703,7 @@ def run_c3(args, world, rank, dev, T, chained):
 
         def step():
             chain.sums()
-            base = tpf_shard.chained_base(chain.total, start0=start0) if world > 1 else start0
+            base = tpf_shard.chained_base(chain.total, start0=start0) if T.dist_on else start0
             chain.decode(base, out=out)
 
         fn = step
@@ -914,8 +914,8 @@ def run_selftest(args, world, rank, dev, T):
         return None
     res = line("selftest (CPU stand-in step, no codec)", 0.0, "none", world, args.steps, args.warmup, elapsed, "int64",
                "synthetic", {"workload": "selftest", "parallelism": f"shard{world}",
-                             "world_size": torch.distributed.get_world_size() if world > 1 else 1,
-                             "backend": torch.distributed.get_backend() if world > 1 else None})
+                             "world_size": torch.distributed.get_world_size() if T.dist_on else 1,
+                             "backend": torch.distributed.get_backend() if T.dist_on else None})
     res["selftest"] = True
     res["per_rank"] = per_rank
     return res, True
@@ -945,7 +945,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
-    dist_on = world > 1
+    # under a launcher (WORLD_SIZE set) the process group is used even at
+    # world size 1, so `torch.distributed.run --nproc-per-node 1` exercises the
+    # RCCL init, barrier, all_gather and all_reduce on a one-GPU box (RCCL
+    # refuses two ranks on one device: "Duplicate GPU detected")
+    dist_on = world > 1 or "WORLD_SIZE" in os.environ
     # Rehearsal of the multi-rank path on a one-GPU box (never the measured
     # configuration): TPF_BENCH_SAME_GPU=1 puts every rank on cuda:0;
     # TPF_BENCH_BACKEND=gloo carries the collectives over gloo instead of RCCL.

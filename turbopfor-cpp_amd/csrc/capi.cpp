@@ -279,7 +279,7 @@ size_t tpf_enc_workspace_size(int fmt, uint64_t nblocks, unsigned n)
 {
     if (fmt == TPF_FMT_256V32 && n == 256)
         return tpf::enc256v32_workspace(nblocks);
-    if (fmt == TPF_FMT_128V64 || fmt == TPF_FMT_256V64)
+    if ((fmt == TPF_FMT_128V64 && n == 128) || fmt == TPF_FMT_256V64)
         return tpf::enc128v64_workspace(nblocks);
     return tpf::generic_workspace(nblocks);
 }
@@ -324,7 +324,7 @@ int tpf_enc_batch(int fmt, const void * d_vals, uint64_t nblocks, unsigned n, in
     if (fmt == TPF_FMT_256V32 && n == 256)
         e = tpf::launch_enc256v32(static_cast<const uint32_t *>(d_vals), nblocks, static_cast<const uint32_t *>(d_starts),
                                   static_cast<uint32_t>(start0), d1 != 0, d_out, out_cap, d_off, d_ws, ws_bytes, s);
-    else if (fmt == TPF_FMT_128V64 || fmt == TPF_FMT_256V64)
+    else if ((fmt == TPF_FMT_128V64 && n == 128) || fmt == TPF_FMT_256V64)
         e = tpf::launch_enc128v64(fmt == TPF_FMT_256V64 ? 2u : 1u, static_cast<const uint64_t *>(d_vals), nblocks, d1 != 0,
                                   static_cast<const uint64_t *>(d_starts), start0, d_out, out_cap, d_off, d_ws, ws_bytes, s);
     else

@@ -93,24 +93,40 @@ void tc(int rc)
 
 // Page-lock (and map) a host range for the duration of a call unless it
 // already is; d = the range's device address (nullptr if the device cannot
-// address it, e.g. registration failed).
+// address it: then the range is left pageable and HIP stages the copies).
+// "Already pinned" needs BOTH ends of the range inside ONE registration: a
+// pageable array that shares its first page with another registered array
+// (malloc'd neighbours) must not be taken for pinned, or a DMA would run past
+// the registered pages.  A range whose end lies in someone else's
+// registration is not registered again (overlapping registrations), it stays
+// pageable.
 struct Pin
 {
     void * p = nullptr;
     void * d = nullptr;
+    static bool lookup(const void * q, hipPointerAttribute_t & a)
+    {
+        a = hipPointerAttribute_t{};
+        const bool ok = hipPointerGetAttributes(&a, q) == hipSuccess && a.type != hipMemoryTypeUnregistered;
+        if (!ok)
+            (void)hipGetLastError();
+        return ok;
+    }
     Pin(const void * ptr, size_t bytes)
     {
         if (!ptr || !bytes)
             return;
-        hipPointerAttribute_t a{};
-        if (hipPointerGetAttributes(&a, ptr) == hipSuccess && a.type != hipMemoryTypeUnregistered)
+        const uint8_t * lo = static_cast<const uint8_t *>(ptr);
+        const uint8_t * hi = lo + bytes - 1;
+        hipPointerAttribute_t a{}, b{};
+        const bool known_lo = lookup(lo, a), known_hi = lookup(hi, b);
+        if (known_lo || known_hi)
         {
-            if (a.type == hipMemoryTypeHost && a.devicePointer && a.hostPointer)
-                d = static_cast<uint8_t *>(a.devicePointer)
-                    + (static_cast<const uint8_t *>(ptr) - static_cast<const uint8_t *>(a.hostPointer));
-            return;
+            if (known_lo && known_hi && a.type == hipMemoryTypeHost && b.type == hipMemoryTypeHost && a.hostPointer &&
+                a.hostPointer == b.hostPointer && a.devicePointer)
+                d = static_cast<uint8_t *>(a.devicePointer) + (lo - static_cast<const uint8_t *>(a.hostPointer));
+            return; // device memory, or not one registration: leave it to HIP
         }
-        (void)hipGetLastError();
         if (hipHostRegister(const_cast<void *>(ptr), bytes, hipHostRegisterMapped) == hipSuccess)
         {
             p = const_cast<void *>(ptr);
