@@ -183,8 +183,6 @@ struct Slot
 {
     hipEvent_t up = nullptr, mid = nullptr, done = nullptr;
     Buf in, vals, ws, start, off, hoff{true};
-    Buf derr, herr{true}; // decode: the chunk's first inconsistent block (device word, pinned copy)
-    uint64_t c0 = ~0ull;  // decode: first block of the chunk the slot last carried (~0: none)
     Slot()
     {
         for (hipEvent_t * e : {&up, &mid, &done})
@@ -203,6 +201,7 @@ struct Pipeline
     int dev = -1;
     hipStream_t cs = nullptr, ks = nullptr; // copy stream, kernel stream
     Slot slots[kSlots];
+    Buf errs; // decode: one first-inconsistent-block word per chunk, read back once at the end
     explicit Pipeline(int d) : dev(d)
     {
         hc(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "stream");
@@ -318,24 +317,16 @@ int tpf_host_dec(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_
         }
         Lease lease;
         Pipeline & P = *lease.p;
-        uint64_t bad = ~0ull; // first block whose parsed length disagrees with its offsets
-        auto collect = [&](Slot & sl) {
-            if (sl.c0 != ~0ull)
-            {
-                const uint64_t e = *static_cast<const uint64_t *>(sl.herr.p);
-                if (e != ~0ull)
-                    bad = std::min(bad, sl.c0 + e);
-            }
-            sl.c0 = ~0ull;
-        };
-        for (Slot & sl : P.slots)
-            sl.c0 = ~0ull;
+        // per chunk, the first block whose parsed length disagrees with its
+        // offsets: a device word each, brought back with ONE copy at the end
+        // (a small device-to-host copy per chunk can stall the host loop)
+        const uint64_t nchunks = (nblocks + chunk - 1) / chunk;
+        auto * d_errs = static_cast<uint64_t *>(P.errs.get(nchunks * 8));
         uint64_t k = 0;
         for (uint64_t c0 = 0; c0 < nblocks; c0 += chunk, ++k)
         {
             Slot & sl = P.slots[k % kSlots];
             hc(hipEventSynchronize(sl.done), "wait slot"); // chunk k-kSlots is done with the slot
-            collect(sl);
             const uint64_t c1 = std::min(nblocks, c0 + chunk);
             const uint64_t nb = c1 - c0;
             const uint64_t b0 = h_off[c0], bytes = h_off[c1] - b0;
@@ -353,20 +344,23 @@ int tpf_host_dec(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_
                    "H2D starts");
             hc(hipEventRecord(sl.up, P.cs), "record up");
             hc(hipStreamWaitEvent(P.ks, sl.up, 0), "wait up");
-            auto * d_err = static_cast<uint64_t *>(sl.derr.get(8));
-            sl.herr.get(8);
-            tc(tpf_dec_batch(fmt, d_in, bytes, d_off, nb, n, out, d_start, d_err, P.ks));
-            hc(hipMemcpyAsync(sl.herr.p, d_err, 8, hipMemcpyDeviceToHost, P.ks), "D2H err");
-            sl.c0 = c0;
+            tc(tpf_dec_batch(fmt, d_in, bytes, d_off, nb, n, out, d_start, d_errs + k, P.ks));
             if (!dv)
                 hc(hipMemcpyAsync(static_cast<uint8_t *>(h_vals) + c0 * uv * es, out, nb * uv * es, hipMemcpyDeviceToHost, P.ks),
                    "D2H vals");
             hc(hipEventRecord(sl.done, P.ks), "record done");
         }
+        std::vector<uint64_t> errs(nchunks);
+        hc(hipMemcpyAsync(errs.data(), d_errs, nchunks * 8, hipMemcpyDeviceToHost, P.ks), "D2H errs");
         hc(hipStreamSynchronize(P.ks), "sync");
         lease.ok = true;
-        for (Slot & sl : P.slots)
-            collect(sl);
+        uint64_t bad = ~0ull; // first block whose parsed length disagrees with its offsets
+        for (uint64_t i = 0; i < nchunks; ++i)
+            if (errs[i] != ~0ull)
+            {
+                bad = i * chunk + errs[i];
+                break;
+            }
         if (bad != ~0ull)
             throw Err(TPF_ECORRUPT, "tpf_host_dec: block " + std::to_string(bad) + " parses to a length other than its offsets");
         return TPF_OK;
