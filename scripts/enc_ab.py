@@ -1,0 +1,61 @@
+"""A/B of the 256v32 encoders on one box (C4 mix, 10M blocks): the production
+single-launch pipelined encoder vs the two-pass one (tpf_probe_enc256v32 mode
+3), alternating, HIP events on the launch stream; both outputs verified."""
+import ctypes
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "turbopfor-cpp_amd", "python"))
+sys.path.insert(0, ROOT)
+import turbopfor_amd as tpf  # noqa: E402
+import bench  # noqa: E402
+
+nb = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+dev = torch.device("cuda:0")
+vals, _ = bench.gen_c2(nb, 0, seed=11, dev=dev, pcts=[0, 5, 10, 25])
+L = tpf.lib()
+cap = int(L.tpf_p4enc256v32_bound(nb))
+out = torch.empty(cap, dtype=torch.uint8, device=dev)
+offs = torch.empty(nb + 1, dtype=torch.int64, device=dev)
+wsb = int(L.tpf_p4enc256v32_workspace_size(nb))
+ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def pipe():
+    assert L.tpf_p4enc256v32_batch(vals.data_ptr(), nb, out.data_ptr(), cap, offs.data_ptr(), ws.data_ptr(), wsb, s) == 0
+
+
+def twopass():
+    assert L.tpf_probe_enc256v32(3, vals.data_ptr(), nb, out.data_ptr(), cap, offs.data_ptr(), ws.data_ptr(), wsb, s) == 0
+
+
+def timed(fn, reps=10):
+    for _ in range(2):
+        fn()
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    e[0].record()
+    for _ in range(reps):
+        fn()
+    e[1].record()
+    torch.cuda.synchronize()
+    return e[0].elapsed_time(e[1]) / reps
+
+
+res = {}
+for fn, name in ((twopass, "twopass"), (pipe, "pipe")):
+    fn()
+    torch.cuda.synchronize()
+    tot = int(offs[-1].item())
+    back = tpf.dec256v32(out[:tot], offs, nb)
+    ok = bool(torch.equal(back, vals))
+    res[name] = (tot, ok)
+    print(name, "total", tot, "verified", ok, flush=True)
+assert res["pipe"][0] == res["twopass"][0]
+for rnd in range(3):
+    for fn, name in ((twopass, "twopass"), (pipe, "pipe")):
+        ms = timed(fn)
+        print(f"round {rnd} {name:8s} {ms:.4f} ms  {nb * 256 / ms / 1e6:.1f} G int32/s", flush=True)

@@ -70,10 +70,19 @@ struct EncRun
 
     __device__ __forceinline__ bool init(const uint32_t * in, uint64_t nblocks, uint32_t wv)
     {
-        first = (static_cast<uint64_t>(blockIdx.x) * 4u + wv) * kEncRun;
+        return init_at(in, nblocks, (static_cast<uint64_t>(blockIdx.x) * 4u + wv) * kEncRun, kEncRun);
+    }
+
+    // run of up to nmax (<= 64) blocks from block `at`
+    __device__ __forceinline__ bool init_at(const uint32_t * in, uint64_t nblocks, uint64_t at, uint32_t nmax)
+    {
+        first = at;
         if (first >= nblocks)
+        {
+            n = 0;
             return false;
-        n = static_cast<uint32_t>(min_u64(kEncRun, nblocks - first));
+        }
+        n = static_cast<uint32_t>(min_u64(nmax, nblocks - first));
         rs = make_rsrc(in + first * 256u, n * 1024u);
         return true;
     }
@@ -126,21 +135,14 @@ __device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t lane)
     return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(lane)));
 }
 
+// Plan a run: lane j of (szv, pwv) = size and plan word of block R.first+j.
 template <bool D1, int PROBE = 0>
-__global__ __launch_bounds__(256) void k_enc256v32_plan(const uint32_t * __restrict in, uint64_t nblocks,
-                                                         const uint32_t * __restrict starts, uint32_t start0,
-                                                         uint64_t * __restrict sizes, uint32_t * __restrict plan)
+__device__ __forceinline__ void plan_run(const EncRun & R, const uint32_t * in, const uint32_t * starts, uint32_t start0,
+                                         uint32_t * hist, uint32_t t, uint32_t & szv, uint32_t & pwv)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t hist[4][kPlanHistU32];
-    const uint32_t t = threadIdx.x & 63u;
-    const uint32_t wv = uni(threadIdx.x >> 6);
-    if (blockIdx.x == 0 && threadIdx.x == 0)
-        sizes[nblocks] = 0; // exclusive scan over nblocks+1 entries yields the total
-    EncRun R;
-    if (!R.init(in, nblocks, wv))
-        return;
     const uint32_t stv = D1 ? R.start_lane(in, starts, start0, t) : 0u;
-    uint32_t szv = 0u, pwv = 0u; // lane j: block first+j
+    szv = 0u;
+    pwv = 0u;
     R.walk(t, [&](u32x4 v, uint32_t jj) {
         if constexpr (D1)
             v = delta_encode(v, rl32(stv, jj), t);
@@ -154,10 +156,62 @@ __global__ __launch_bounds__(256) void k_enc256v32_plan(const uint32_t * __restr
             P.raw = 0;
         }
         else
-            P = plan_block256(v, hist[wv], t);
+            P = plan_block256(v, hist, t);
         szv = t == jj ? P.size : szv;
         pwv = t == jj ? plan_word(P) : pwv;
     });
+}
+
+// Write a run: lane j of (szv, pwv, olo/ohi) = size, plan word and byte
+// offset of block R.first+j.  img: the wave's zeroed LDS image (left zeroed).
+template <bool D1, int PROBE = 0>
+__device__ __forceinline__ void write_run(const EncRun & R, const uint32_t * in, const uint32_t * starts, uint32_t start0,
+                                          uint32_t szv, uint32_t pwv, uint32_t olo, uint32_t ohi, uint32_t * img,
+                                          uint32_t * val, uint64_t out_base, uint64_t cap_end, uint32_t t)
+{
+    const uint32_t stv = D1 ? R.start_lane(in, starts, start0, t) : 0u;
+    R.walk(t, [&](u32x4 v, uint32_t jj) {
+        if constexpr (D1)
+            v = delta_encode(v, rl32(stv, jj), t);
+        const uint32_t size = rl32(szv, jj);
+        const Plan32 P = unplan(rl32(pwv, jj), size);
+        const uint64_t dst = out_base + ((static_cast<uint64_t>(rl32(ohi, jj)) << 32) | rl32(olo, jj));
+        if constexpr (PROBE == 2)
+        {
+            reinterpret_cast<u32x4 *>(img)[4 + t] = v;
+            wave_lds_sync();
+            copy_out_image16(img, kImgLead, dst, size, cap_end, t);
+            wave_lds_sync();
+            zero_image(img, kImgU32 / 4u, t);
+            wave_lds_sync();
+            return;
+        }
+        const uint32_t sb = emit_block256<true>(img, val, P, v, t);
+        wave_lds_sync();
+        copy_out_image16(img, sb, dst, size, cap_end, t);
+        wave_lds_sync();
+        // only [0, sb + size) can be non-zero: clear it for the next block
+        zero_image(img, min((sb + size + 15u) >> 4, kImgU32 / 4u), t);
+        wave_lds_sync();
+    });
+}
+
+// ---- two-pass encoder (plan -> hipcub scan -> write): kept for A/B ---------
+template <bool D1, int PROBE = 0>
+__global__ __launch_bounds__(256) void k_enc256v32_plan(const uint32_t * __restrict in, uint64_t nblocks,
+                                                         const uint32_t * __restrict starts, uint32_t start0,
+                                                         uint64_t * __restrict sizes, uint32_t * __restrict plan)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t hist[4][kPlanHistU32];
+    const uint32_t t = threadIdx.x & 63u;
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        sizes[nblocks] = 0; // exclusive scan over nblocks+1 entries yields the total
+    EncRun R;
+    if (!R.init(in, nblocks, wv))
+        return;
+    uint32_t szv, pwv; // lane j: block first+j
+    plan_run<D1, PROBE>(R, in, starts, start0, hist[wv], t, szv, pwv);
     if (t < R.n)
     {
         sizes[R.first + t] = szv;
@@ -179,39 +233,255 @@ __global__ __launch_bounds__(256) void k_enc256v32_write(const uint32_t * __rest
     EncRun R;
     if (!R.init(in, nblocks, wv))
         return;
-    const uint32_t stv = D1 ? R.start_lane(in, starts, start0, t) : 0u;
     // lane j: destination offset (64-bit), size and plan of block first+j
     const uint64_t ov = t < R.n ? off[R.first + t] : 0ull;
     const uint64_t ev = t < R.n ? off[R.first + t + 1u] : 0ull;
     const uint32_t szv = static_cast<uint32_t>(ev - ov);
     const uint32_t pwv = t < R.n ? plan[R.first + t] : 0u;
-    const uint32_t olo = static_cast<uint32_t>(ov), ohi = static_cast<uint32_t>(ov >> 32);
+    zero_image(img, kImgU32 / 4u, t);
+    wave_lds_sync();
+    const uint64_t out_base = reinterpret_cast<uint64_t>(out);
+    write_run<D1, PROBE>(R, in, starts, start0, szv, pwv, static_cast<uint32_t>(ov), static_cast<uint32_t>(ov >> 32), img,
+                         val_all[wv], out_base, out_base + out_cap, t);
+}
+
+// ---- single-launch pipelined encoder ---------------------------------------
+// The blocks are cut into chunks of kPipeChunkItems workgroup items of
+// kPipeItem blocks (4 waves x kPipeRun).  ONE persistent launch walks a fixed
+// sequence of items, step s = [plan items of chunk s] interleaved with
+// [write items of chunk s - 1]:
+//   plan item  : plans its 128 blocks (p4Bits32 cost model), publishes each
+//                block's size and plan word, its runs' and its own byte
+//                totals, and arrives on the chunk's counter; the LAST arriving
+//                item scans the chunk's item totals (item offsets inside the
+//                chunk), chains the chunk's byte offset from the previous
+//                chunk's and flags the chunk ready;
+//   write item : waits for its chunk's flag, derives every block's byte
+//                offset (chunk offset + item offset + run offset + in-run scan),
+//                writes d_off and builds the blocks exactly as the two-pass
+//                write kernel does.
+// A chunk's values (64 MiB) are re-read by its write items one step after its
+// plan items read them, while the 256 MiB Infinity Cache still holds them, so
+// the second read costs no HBM traffic (the two-pass encoder re-reads all
+// values from HBM: 1.33x algorithmic traffic, profiles/pmc_traffic.json c4),
+// the offset scan needs no extra launch, and the compute-heavy planning of
+// one chunk runs beside the memory-heavy writing of the previous one.
+// Hand-offs (MI355X_MICROARCH.md "visibility", cdna_hip_programming.md G16):
+// every published word is stored write-through (agent-scope relaxed atomic
+// store = sc1) and drained (s_waitcnt vmcnt(0)) by every storing wave before
+// the workgroup barrier and the counter add / flag store; consumers poll one
+// word relaxed with s_sleep, take ONE agent-scope acquire and read the
+// published words with sc1 loads.  Deadlock-free with every workgroup
+// resident (grid sized from the occupancy query, one workgroup per CU
+// spare): a write item waits only for plan items of an EARLIER step and the
+// last arriver of chunk c only for chunk c-1's flag, so the earliest
+// unfinished item of the sequence can always proceed.  Every wait is bounded
+// (kSpinLimit polls): on expiry the kernel raises an abort word and a finish
+// kernel stores UINT64_MAX in d_off[nblocks].
+constexpr uint32_t kPipeRun = 32;
+constexpr uint32_t kPipeItem = 4u * kPipeRun;
+constexpr uint32_t kPipeChunkItems = 512; // 64K blocks = 64 MiB of values per chunk
+constexpr uint32_t kSpinLimit = 1u << 22; // polls of ~0.2 us
+
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) uint64_t gu64;
+
+__device__ __forceinline__ void st_wt(uint32_t * p, uint32_t v)
+{
+    __hip_atomic_store((gu32 *)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt64(uint64_t * p, uint64_t v)
+{
+    __hip_atomic_store((gu64 *)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_wt(const uint32_t * p)
+{
+    return __hip_atomic_load((gu32 *)(const_cast<uint32_t *>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_wt64(const uint64_t * p)
+{
+    return __hip_atomic_load((gu64 *)(const_cast<uint64_t *>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Workspace of the pipelined encoder.  The polled words (count, ready,
+// abort) sit first, in one 16-byte-padded block zeroed before every launch.
+struct PipeWs
+{
+    uint32_t * count; // [nchunks] arrivals of plan items
+    uint32_t * ready; // [nchunks] chunk scanned and chained
+    uint32_t * abort; // [4] bounded-wait expiry
+    uint64_t * cbase; // [nchunks] byte offset of the chunk
+    uint64_t * ctot;  // [nchunks] byte total of the chunk
+    uint32_t * itot;  // [nitems] byte total of an item
+    uint32_t * ibase; // [nitems] byte offset of an item inside its chunk
+    uint32_t * rtot;  // [nitems * 4] byte total of a run
+    uint32_t * sz;    // [nblocks] block sizes
+    uint32_t * plan;  // [nblocks] plan words
+};
+
+// Bounded wait (whole wave, uniform) until *flag != 0; false on expiry or abort.
+__device__ __forceinline__ bool wait_set(const uint32_t * flag, uint32_t * abort)
+{
+    for (uint32_t n = 0;; ++n)
+    {
+        if (uni(ld_wt(flag)) != 0u)
+            return true;
+        if (uni(ld_wt(abort)) != 0u)
+            return false;
+        if (n >= kSpinLimit)
+        {
+            st_wt(abort, 1u);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
+template <bool D1>
+__global__ __launch_bounds__(256) void k_enc256v32_pipe(const uint32_t * __restrict in, uint64_t nblocks,
+                                                         const uint32_t * __restrict starts, uint32_t start0,
+                                                         uint8_t * __restrict out, uint64_t out_cap, uint64_t * __restrict off,
+                                                         PipeWs W, uint32_t nchunks, uint64_t nitems)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t hist[4][kPlanHistU32];
+    __shared__ __attribute__((aligned(16))) uint32_t img_all[4][kImgU32];
+    __shared__ __attribute__((aligned(16))) uint32_t val_all[4][kEncValU32];
+    __shared__ uint32_t xch[16];
+    const uint32_t t = threadIdx.x & 63u;
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    uint32_t * img = img_all[wv];
     const uint64_t out_base = reinterpret_cast<uint64_t>(out);
     const uint64_t cap_end = out_base + out_cap;
     zero_image(img, kImgU32 / 4u, t);
     wave_lds_sync();
-    R.walk(t, [&](u32x4 v, uint32_t jj) {
-        if constexpr (D1)
-            v = delta_encode(v, rl32(stv, jj), t);
-        const uint32_t size = rl32(szv, jj);
-        const Plan32 P = unplan(rl32(pwv, jj), size);
-        const uint64_t dst = out_base + ((static_cast<uint64_t>(rl32(ohi, jj)) << 32) | rl32(olo, jj));
-        if constexpr (PROBE == 2)
+    const uint64_t nseq = static_cast<uint64_t>(nchunks + 1u) * (2u * kPipeChunkItems);
+    uint32_t witem = 0; // write items seen by this workgroup (uniform)
+    for (uint64_t q = blockIdx.x; q < nseq; q += gridDim.x)
+    {
+        const uint32_t step = static_cast<uint32_t>(q / (2u * kPipeChunkItems));
+        const uint32_t r = static_cast<uint32_t>(q % (2u * kPipeChunkItems));
+        const bool is_plan = (r & 1u) == 0u;
+        const uint32_t c = is_plan ? step : step - 1u; // write items lag one step
+        if (!is_plan && step == 0u)
+            continue;
+        if (c >= nchunks)
+            continue;
+        const uint64_t item = static_cast<uint64_t>(c) * kPipeChunkItems + (r >> 1);
+        if (item >= nitems)
+            continue;
+        const uint32_t citems = static_cast<uint32_t>(min_u64(kPipeChunkItems, nitems - static_cast<uint64_t>(c) * kPipeChunkItems));
+        const uint64_t run = item * 4u + wv;
+        EncRun R;
+        R.init_at(in, nblocks, run * kPipeRun, kPipeRun);
+        if (is_plan)
         {
-            reinterpret_cast<u32x4 *>(img)[4 + t] = v;
-            wave_lds_sync();
-            copy_out_image16(img, kImgLead, dst, size, cap_end, t);
-            wave_lds_sync();
-            return;
+            // ---- plan item: sizes + plan words, run / item totals, arrival
+            uint32_t szv = 0u, pwv = 0u;
+            if (R.n)
+                plan_run<D1>(R, in, starts, start0, hist[wv], t, szv, pwv);
+            if (t < R.n)
+            {
+                st_wt(W.sz + R.first + t, szv);
+                st_wt(W.plan + R.first + t, pwv);
+            }
+            const uint32_t rt = wave_sum(t < R.n ? szv : 0u);
+            if (t == 0)
+            {
+                st_wt(W.rtot + run, rt);
+                xch[wv] = rt;
+            }
+            drain_stores(); // every storing wave, before the barrier that precedes the arrival
+            __syncthreads();
+            if (threadIdx.x == 0)
+            {
+                const uint32_t it = xch[0] + xch[1] + xch[2] + xch[3];
+                st_wt(W.itot + item, it);
+                drain_stores();
+                const uint32_t old = __hip_atomic_fetch_add((gu32 *)(W.count + c), 1u, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+                xch[4] = (old + 1u == citems) ? 1u : 0u;
+            }
+            __syncthreads();
+            if (xch[4] == 0u)
+                continue;
+            // ---- last arriver of chunk c: scan the item totals, chain the chunk offset
+            if (threadIdx.x == 0)
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            drain_stores();
+            __syncthreads();
+            const uint64_t i0 = static_cast<uint64_t>(c) * kPipeChunkItems;
+            const uint32_t ia = 2u * threadIdx.x, ib = ia + 1u; // kPipeChunkItems == 2 * 256
+            const uint32_t a = ia < citems ? ld_wt(W.itot + i0 + ia) : 0u;
+            const uint32_t b = ib < citems ? ld_wt(W.itot + i0 + ib) : 0u;
+            const uint32_t incl = wave_incl_scan(a + b);
+            if (t == 63)
+                xch[8 + wv] = incl;
+            __syncthreads();
+            uint32_t before = 0u;
+            for (uint32_t w = 0; w < wv; ++w)
+                before += xch[8 + w];
+            const uint32_t ex = before + incl - (a + b);
+            if (ia < citems)
+                st_wt(W.ibase + i0 + ia, ex);
+            if (ib < citems)
+                st_wt(W.ibase + i0 + ib, ex + a);
+            if (threadIdx.x == 0)
+            {
+                const uint64_t ctot = static_cast<uint64_t>(xch[8]) + xch[9] + xch[10] + xch[11];
+                uint64_t cb = 0u;
+                bool ok = true;
+                if (c > 0u)
+                {
+                    ok = wait_set(W.ready + (c - 1u), W.abort); // chunk c-1 is an earlier step: never circular
+                    cb = ld_wt64(W.cbase + (c - 1u)) + ld_wt64(W.ctot + (c - 1u));
+                }
+                st_wt64(W.cbase + c, cb);
+                st_wt64(W.ctot + c, ctot);
+                if (c + 1u == nchunks)
+                    off[nblocks] = ok ? cb + ctot : ~0ull;
+            }
+            drain_stores();
+            __syncthreads();
+            if (threadIdx.x == 0)
+                st_wt(W.ready + c, 1u);
         }
-        const uint32_t sb = emit_block256<true>(img, val_all[wv], P, v, t);
-        wave_lds_sync();
-        copy_out_image16(img, sb, dst, size, cap_end, t);
-        wave_lds_sync();
-        // only [0, sb + size) can be non-zero: clear it for the next block
-        zero_image(img, min((sb + size + 15u) >> 4, kImgU32 / 4u), t);
-        wave_lds_sync();
-    });
+        else
+        {
+            // ---- write item: wait for the chunk, derive offsets, build blocks
+            // (the verdict word alternates between two LDS slots: thread 0 may
+            // write the next write item's before a slow wave has read this one)
+            const uint32_t slot = 5u + (witem++ & 1u);
+            if (threadIdx.x == 0)
+            {
+                xch[slot] = wait_set(W.ready + c, W.abort) ? 1u : 0u;
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            }
+            drain_stores();
+            __syncthreads();
+            if (xch[slot] == 0u)
+                continue;
+            if (!R.n)
+                continue;
+            uint64_t rb = ld_wt64(W.cbase + c) + ld_wt(W.ibase + item);
+            for (uint32_t w = 0; w < wv; ++w)
+                rb += ld_wt(W.rtot + item * 4u + w);
+            const uint32_t szv = t < R.n ? ld_wt(W.sz + R.first + t) : 0u;
+            const uint32_t pwv = t < R.n ? ld_wt(W.plan + R.first + t) : 0u;
+            const uint64_t ov = rb + (wave_incl_scan(szv) - szv);
+            if (t < R.n)
+                off[R.first + t] = ov;
+            write_run<D1>(R, in, starts, start0, szv, pwv, static_cast<uint32_t>(ov), static_cast<uint32_t>(ov >> 32), img,
+                          val_all[wv], out_base, cap_end, t);
+        }
+    }
+}
+
+// Abort of the pipelined encoder (a bounded wait expired): mark the stream invalid.
+__global__ void k_enc_pipe_finish(const uint32_t * abort, uint64_t * off, uint64_t nblocks)
+{
+    if (threadIdx.x == 0 && *abort != 0u)
+        off[nblocks] = ~0ull;
 }
 
 } // namespace tpf::dev
@@ -219,13 +489,106 @@ __global__ __launch_bounds__(256) void k_enc256v32_write(const uint32_t * __rest
 namespace tpf
 {
 
-size_t enc256v32_workspace(uint64_t nblocks)
+namespace
+{
+
+size_t al256(size_t x) { return (x + 255u) & ~size_t(255); }
+
+// two-pass encoder workspace: plan words + hipcub scan temp
+size_t twopass_workspace(uint64_t nblocks)
 {
     size_t scan_bytes = 0;
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, static_cast<uint64_t *>(nullptr),
                                      static_cast<int>(std::min<uint64_t>(nblocks + 1, 0x7FFFFFFF)));
-    return ((nblocks * 4u + 255u) & ~size_t(255)) + scan_bytes + 256;
+    return al256(nblocks * 4u) + scan_bytes + 256;
 }
+
+struct PipeGeom
+{
+    uint64_t nitems, nchunks;
+    size_t polled; // bytes of the zeroed block (16-B multiple)
+    size_t bytes;
+};
+
+PipeGeom pipe_geom(uint64_t nblocks)
+{
+    PipeGeom g;
+    g.nitems = (nblocks + dev::kPipeItem - 1) / dev::kPipeItem;
+    g.nchunks = (g.nitems + dev::kPipeChunkItems - 1) / dev::kPipeChunkItems;
+    g.polled = ((g.nchunks * 2u + 4u) * 4u + 15u) & ~size_t(15);
+    g.bytes = al256(g.polled) + 2u * al256(g.nchunks * 8u) + 2u * al256(g.nitems * 4u) + al256(g.nitems * 16u)
+              + 2u * al256(nblocks * 4u);
+    return g;
+}
+
+dev::PipeWs pipe_ws(void * ws, uint64_t nblocks, const PipeGeom & g)
+{
+    uint8_t * p = static_cast<uint8_t *>(ws);
+    dev::PipeWs W;
+    W.count = reinterpret_cast<uint32_t *>(p);
+    W.ready = W.count + g.nchunks;
+    W.abort = W.ready + g.nchunks;
+    p += al256(g.polled);
+    W.cbase = reinterpret_cast<uint64_t *>(p);
+    p += al256(g.nchunks * 8u);
+    W.ctot = reinterpret_cast<uint64_t *>(p);
+    p += al256(g.nchunks * 8u);
+    W.itot = reinterpret_cast<uint32_t *>(p);
+    p += al256(g.nitems * 4u);
+    W.ibase = reinterpret_cast<uint32_t *>(p);
+    p += al256(g.nitems * 4u);
+    W.rtot = reinterpret_cast<uint32_t *>(p);
+    p += al256(g.nitems * 16u);
+    W.sz = reinterpret_cast<uint32_t *>(p);
+    p += al256(nblocks * 4u);
+    W.plan = reinterpret_cast<uint32_t *>(p);
+    return W;
+}
+
+// Workgroups of the persistent grid: every one must be resident at once
+// (the items wait on each other).  The occupancy answer can be one workgroup
+// per CU high (MI355X_MICROARCH.md, residency), so one per CU is left spare.
+template <bool D1>
+uint32_t pipe_grid(uint64_t nitems)
+{
+    static int per_cu[2][64] = {};
+    int dev_id = 0;
+    (void)hipGetDevice(&dev_id);
+    dev_id = dev_id < 0 || dev_id >= 64 ? 0 : dev_id;
+    if (per_cu[D1][dev_id] == 0)
+    {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void *>(dev::k_enc256v32_pipe<D1>), 256, 0)
+                != hipSuccess
+            || n <= 0)
+            n = 1;
+        per_cu[D1][dev_id] = n > 1 ? n - 1 : 1;
+    }
+    const uint64_t want = 2u * nitems; // more workgroups than items would only idle
+    return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want, grid_cap(nullptr, per_cu[D1][dev_id]))));
+}
+
+template <bool D1>
+hipError_t launch_pipe(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, uint8_t * out, uint64_t out_cap,
+                       uint64_t * off, void * ws, hipStream_t stream)
+{
+    const PipeGeom g = pipe_geom(nblocks);
+    const dev::PipeWs W = pipe_ws(ws, nblocks, g);
+    hipError_t e = hipMemsetAsync(W.count, 0, g.polled, stream);
+    if (e != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(dev::k_enc256v32_pipe<D1>, dim3(pipe_grid<D1>(g.nitems)), dim3(256), 0, stream, in, nblocks, starts,
+                       start0, out, out_cap, off, W, static_cast<uint32_t>(g.nchunks), g.nitems);
+    e = hipGetLastError();
+    if (e != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(dev::k_enc_pipe_finish, dim3(1), dim3(64), 0, stream, W.abort, off, nblocks);
+    return hipGetLastError();
+}
+
+} // namespace
+
+size_t enc256v32_workspace(uint64_t nblocks) { return std::max(twopass_workspace(nblocks), pipe_geom(nblocks).bytes); }
 
 hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, bool d1,
                             uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t stream,
@@ -235,8 +598,12 @@ hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_
         return hipMemsetAsync(off, 0, sizeof(uint64_t), stream);
     if (nblocks + 1 > 0x7FFFFFFFull)
         return hipErrorInvalidValue;
+    if (probe == 0)
+        return d1 ? launch_pipe<true>(in, nblocks, starts, start0, out, out_cap, off, ws, stream)
+                  : launch_pipe<false>(in, nblocks, starts, start0, out, out_cap, off, ws, stream);
+    // probe 1 / 2: the two-pass passes with the coding removed; 3: the two-pass encoder itself (A/B)
     uint32_t * plan = static_cast<uint32_t *>(ws);
-    const size_t plan_bytes = (nblocks * 4u + 255u) & ~size_t(255);
+    const size_t plan_bytes = al256(nblocks * 4u);
     void * scan_tmp = static_cast<uint8_t *>(ws) + plan_bytes;
     size_t scan_bytes = ws_bytes > plan_bytes ? ws_bytes - plan_bytes : 0;
     const uint64_t per_wg = 4ull * dev::kEncRun;
