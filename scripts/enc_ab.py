@@ -29,8 +29,18 @@ def pipe():
     assert L.tpf_p4enc256v32_batch(vals.data_ptr(), nb, out.data_ptr(), cap, offs.data_ptr(), ws.data_ptr(), wsb, s) == 0
 
 
-def twopass():
-    assert L.tpf_probe_enc256v32(3, vals.data_ptr(), nb, out.data_ptr(), cap, offs.data_ptr(), ws.data_ptr(), wsb, s) == 0
+def probe(mode):
+    def f():
+        assert L.tpf_probe_enc256v32(mode, vals.data_ptr(), nb, out.data_ptr(), cap, offs.data_ptr(), ws.data_ptr(), wsb,
+                                     s) == 0
+    return f
+
+
+twopass = probe(3)
+# pipelined variants: 16 + chunk items + 1024 * lag + 65536 * (7 waves/SIMD bound)
+VARIANTS = [("twopass", twopass), ("pipe", pipe)] + [
+    (f"ci{ci}_lag{lag}_w{w}", probe(16 + ci + 1024 * lag + 65536 * (w == 7)))
+    for ci, lag, w in [(256, 1, 8), (256, 3, 8), (128, 2, 8), (128, 4, 8), (512, 1, 8), (256, 2, 7)]]
 
 
 def timed(fn, reps=10):
@@ -46,7 +56,8 @@ def timed(fn, reps=10):
 
 
 res = {}
-for fn, name in ((twopass, "twopass"), (pipe, "pipe")):
+for name, fn in VARIANTS:
+    out.zero_()
     fn()
     torch.cuda.synchronize()
     tot = int(offs[-1].item())
@@ -54,8 +65,8 @@ for fn, name in ((twopass, "twopass"), (pipe, "pipe")):
     ok = bool(torch.equal(back, vals))
     res[name] = (tot, ok)
     print(name, "total", tot, "verified", ok, flush=True)
-assert res["pipe"][0] == res["twopass"][0]
-for rnd in range(3):
-    for fn, name in ((twopass, "twopass"), (pipe, "pipe")):
+    assert ok and tot == res["twopass"][0], name
+for rnd in range(2):
+    for name, fn in VARIANTS:
         ms = timed(fn)
-        print(f"round {rnd} {name:8s} {ms:.4f} ms  {nb * 256 / ms / 1e6:.1f} G int32/s", flush=True)
+        print(f"round {rnd} {name:16s} {ms:.4f} ms  {nb * 256 / ms / 1e6:.1f} G int32/s", flush=True)

@@ -280,8 +280,11 @@ __global__ __launch_bounds__(256) void k_enc256v32_write(const uint32_t * __rest
 // kernel stores UINT64_MAX in d_off[nblocks].
 constexpr uint32_t kPipeRun = 32;
 constexpr uint32_t kPipeItem = 4u * kPipeRun;
-constexpr uint32_t kPipeChunkItems = 512; // 64K blocks = 64 MiB of values per chunk
-constexpr uint32_t kSpinLimit = 1u << 22; // polls of ~0.2 us
+constexpr uint32_t kPipeMaxChunkItems = 512; // the last arriver's scan covers 2 items per thread
+constexpr uint32_t kPipeChunkItems = 256;    // default: 32K blocks = 32 MiB of values per chunk
+constexpr uint32_t kPipeLag = 2;             // default: chunk c is written in step c + 2
+constexpr int kPipeMinWaves = 8;             // default launch bound: 8 waves per SIMD
+constexpr uint32_t kSpinLimit = 1u << 22;    // polls of ~0.2 us
 
 typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef __attribute__((address_space(1))) uint64_t gu64;
@@ -304,13 +307,15 @@ __device__ __forceinline__ uint64_t ld_wt64(const uint64_t * p)
 }
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Workspace of the pipelined encoder.  The polled words (count, ready,
-// abort) sit first, in one 16-byte-padded block zeroed before every launch.
+// Workspace of the pipelined encoder.  The polled words (ticket head,
+// counters, flags, abort) sit first, in one 16-byte-padded block zeroed
+// before every launch.
 struct PipeWs
 {
+    uint32_t * head;  // [4] ticket counter (word 0)
+    uint32_t * abort; // [4] bounded-wait expiry (word 0)
     uint32_t * count; // [nchunks] arrivals of plan items
     uint32_t * ready; // [nchunks] chunk scanned and chained
-    uint32_t * abort; // [4] bounded-wait expiry
     uint64_t * cbase; // [nchunks] byte offset of the chunk
     uint64_t * ctot;  // [nchunks] byte total of the chunk
     uint32_t * itot;  // [nitems] byte total of an item
@@ -320,14 +325,14 @@ struct PipeWs
     uint32_t * plan;  // [nblocks] plan words
 };
 
-// Bounded wait (whole wave, uniform) until *flag != 0; false on expiry or abort.
+// Bounded wait (one lane) until *flag != 0; false on expiry or abort.
 __device__ __forceinline__ bool wait_set(const uint32_t * flag, uint32_t * abort)
 {
     for (uint32_t n = 0;; ++n)
     {
-        if (uni(ld_wt(flag)) != 0u)
+        if (ld_wt(flag) != 0u)
             return true;
-        if (uni(ld_wt(abort)) != 0u)
+        if (ld_wt(abort) != 0u)
             return false;
         if (n >= kSpinLimit)
         {
@@ -338,11 +343,128 @@ __device__ __forceinline__ bool wait_set(const uint32_t * flag, uint32_t * abort
     }
 }
 
+struct PipeArgs
+{
+    const uint32_t * in;
+    uint64_t nblocks;
+    const uint32_t * starts;
+    uint32_t start0;
+    uint64_t out_base, cap_end;
+    uint64_t * off;
+    uint64_t nitems;
+    uint32_t nchunks, ci, lag;
+};
+
+// Plan item: plan 4 runs of kPipeRun blocks, publish sizes / plan words / run
+// and item totals (write-through, drained), arrive on the chunk counter; the
+// last arriver scans the chunk's item totals and chains the chunk offset.
 template <bool D1>
-__global__ __launch_bounds__(256) void k_enc256v32_pipe(const uint32_t * __restrict in, uint64_t nblocks,
-                                                         const uint32_t * __restrict starts, uint32_t start0,
-                                                         uint8_t * __restrict out, uint64_t out_cap, uint64_t * __restrict off,
-                                                         PipeWs W, uint32_t nchunks, uint64_t nitems)
+__device__ __forceinline__ void pipe_plan(const PipeArgs & A, const PipeWs & W, uint32_t c, uint64_t item, uint32_t citems,
+                                          uint32_t * hist, uint32_t * xch, uint32_t t, uint32_t wv)
+{
+    const uint64_t run = item * 4u + wv;
+    EncRun R;
+    R.init_at(A.in, A.nblocks, run * kPipeRun, kPipeRun);
+    uint32_t szv = 0u, pwv = 0u;
+    if (R.n)
+        plan_run<D1>(R, A.in, A.starts, A.start0, hist, t, szv, pwv);
+    if (t < R.n)
+    {
+        st_wt(W.sz + R.first + t, szv);
+        st_wt(W.plan + R.first + t, pwv);
+    }
+    const uint32_t rt = wave_sum(t < R.n ? szv : 0u);
+    if (t == 0)
+    {
+        st_wt(W.rtot + run, rt);
+        xch[wv] = rt;
+    }
+    drain_stores(); // every storing wave, before the barrier in front of the arrival
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        st_wt(W.itot + item, xch[0] + xch[1] + xch[2] + xch[3]);
+        drain_stores();
+        const uint32_t old = __hip_atomic_fetch_add((gu32 *)(W.count + c), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        xch[4] = (old + 1u == citems) ? 1u : 0u;
+        if (xch[4])
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    drain_stores();
+    __syncthreads();
+    if (xch[4] == 0u)
+        return;
+    // last arriver of chunk c: exclusive scan of the item totals (<= 2 per thread)
+    const uint64_t i0 = static_cast<uint64_t>(c) * A.ci;
+    const uint32_t ia = 2u * threadIdx.x, ib = ia + 1u;
+    const uint32_t a = ia < citems ? ld_wt(W.itot + i0 + ia) : 0u;
+    const uint32_t b = ib < citems ? ld_wt(W.itot + i0 + ib) : 0u;
+    const uint32_t incl = wave_incl_scan(a + b);
+    if (t == 63)
+        xch[8 + wv] = incl;
+    __syncthreads();
+    uint32_t before = 0u;
+    for (uint32_t w = 0; w < wv; ++w)
+        before += xch[8 + w];
+    const uint32_t ex = before + incl - (a + b);
+    if (ia < citems)
+        st_wt(W.ibase + i0 + ia, ex);
+    if (ib < citems)
+        st_wt(W.ibase + i0 + ib, ex + a);
+    if (threadIdx.x == 0)
+    {
+        const uint64_t ctot = static_cast<uint64_t>(xch[8]) + xch[9] + xch[10] + xch[11];
+        uint64_t cb = 0u;
+        bool ok = true;
+        if (c > 0u)
+        {
+            // chunk c-1's plan items hold earlier tickets: their last arriver is running or done
+            ok = wait_set(W.ready + (c - 1u), W.abort);
+            cb = ld_wt64(W.cbase + (c - 1u)) + ld_wt64(W.ctot + (c - 1u));
+        }
+        st_wt64(W.cbase + c, cb);
+        st_wt64(W.ctot + c, ctot);
+        if (c + 1u == A.nchunks)
+            A.off[A.nblocks] = ok ? cb + ctot : ~0ull;
+    }
+    drain_stores();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        st_wt(W.ready + c, 1u);
+}
+
+// Write item: wait for the chunk, derive every block's offset, build the blocks.
+template <bool D1>
+__device__ __forceinline__ void pipe_write(const PipeArgs & A, const PipeWs & W, uint32_t c, uint64_t item, uint32_t * img,
+                                           uint32_t * val, uint32_t * xch, uint32_t t, uint32_t wv)
+{
+    if (threadIdx.x == 0)
+    {
+        xch[5] = wait_set(W.ready + c, W.abort) ? 1u : 0u;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    drain_stores();
+    __syncthreads();
+    if (xch[5] == 0u)
+        return;
+    const uint64_t run = item * 4u + wv;
+    EncRun R;
+    if (!R.init_at(A.in, A.nblocks, run * kPipeRun, kPipeRun))
+        return;
+    uint64_t rb = ld_wt64(W.cbase + c) + ld_wt(W.ibase + item);
+    for (uint32_t w = 0; w < wv; ++w)
+        rb += ld_wt(W.rtot + item * 4u + w);
+    const uint32_t szv = t < R.n ? ld_wt(W.sz + R.first + t) : 0u;
+    const uint32_t pwv = t < R.n ? ld_wt(W.plan + R.first + t) : 0u;
+    const uint64_t ov = rb + (wave_incl_scan(szv) - szv);
+    if (t < R.n)
+        A.off[R.first + t] = ov;
+    write_run<D1>(R, A.in, A.starts, A.start0, szv, pwv, static_cast<uint32_t>(ov), static_cast<uint32_t>(ov >> 32), img, val,
+                  A.out_base, A.cap_end, t);
+}
+
+template <bool D1, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_enc256v32_pipe(PipeArgs A, PipeWs W)
 {
     __shared__ __attribute__((aligned(16))) uint32_t hist[4][kPlanHistU32];
     __shared__ __attribute__((aligned(16))) uint32_t img_all[4][kImgU32];
@@ -351,129 +473,44 @@ __global__ __launch_bounds__(256) void k_enc256v32_pipe(const uint32_t * __restr
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
     uint32_t * img = img_all[wv];
-    const uint64_t out_base = reinterpret_cast<uint64_t>(out);
-    const uint64_t cap_end = out_base + out_cap;
     zero_image(img, kImgU32 / 4u, t);
     wave_lds_sync();
-    const uint64_t nseq = static_cast<uint64_t>(nchunks + 1u) * (2u * kPipeChunkItems);
-    uint32_t witem = 0; // write items seen by this workgroup (uniform)
-    for (uint64_t q = blockIdx.x; q < nseq; q += gridDim.x)
+    const uint32_t nseq = (A.nchunks + A.lag) * (2u * A.ci);
+    // Items come from a ticket counter, in sequence order, and every
+    // workgroup runs its tickets in order: a write item then waits only on
+    // plan items that running workgroups hold, so there is no residency
+    // assumption (a static item -> workgroup map would need every workgroup
+    // resident).  The next ticket is taken while the current item runs.
+    if (threadIdx.x == 0)
+        xch[12] = __hip_atomic_fetch_add((gu32 *)W.head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    uint32_t q = xch[12];
+    for (uint32_t it = 0; q < nseq; ++it)
     {
-        const uint32_t step = static_cast<uint32_t>(q / (2u * kPipeChunkItems));
-        const uint32_t r = static_cast<uint32_t>(q % (2u * kPipeChunkItems));
+        const uint32_t nslot = 12u + ((it + 1u) & 1u);
+        if (threadIdx.x == 0)
+            xch[nslot] = __hip_atomic_fetch_add((gu32 *)W.head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // sequence: step s = plan items of chunk s interleaved with write items of chunk s - lag
+        const uint32_t step = q / (2u * A.ci);
+        const uint32_t r = q % (2u * A.ci);
         const bool is_plan = (r & 1u) == 0u;
-        const uint32_t c = is_plan ? step : step - 1u; // write items lag one step
-        if (!is_plan && step == 0u)
-            continue;
-        if (c >= nchunks)
-            continue;
-        const uint64_t item = static_cast<uint64_t>(c) * kPipeChunkItems + (r >> 1);
-        if (item >= nitems)
-            continue;
-        const uint32_t citems = static_cast<uint32_t>(min_u64(kPipeChunkItems, nitems - static_cast<uint64_t>(c) * kPipeChunkItems));
-        const uint64_t run = item * 4u + wv;
-        EncRun R;
-        R.init_at(in, nblocks, run * kPipeRun, kPipeRun);
-        if (is_plan)
+        if (is_plan || step >= A.lag)
         {
-            // ---- plan item: sizes + plan words, run / item totals, arrival
-            uint32_t szv = 0u, pwv = 0u;
-            if (R.n)
-                plan_run<D1>(R, in, starts, start0, hist[wv], t, szv, pwv);
-            if (t < R.n)
+            const uint32_t c = is_plan ? step : step - A.lag;
+            const uint64_t item = static_cast<uint64_t>(c) * A.ci + (r >> 1);
+            if (c < A.nchunks && item < A.nitems)
             {
-                st_wt(W.sz + R.first + t, szv);
-                st_wt(W.plan + R.first + t, pwv);
-            }
-            const uint32_t rt = wave_sum(t < R.n ? szv : 0u);
-            if (t == 0)
-            {
-                st_wt(W.rtot + run, rt);
-                xch[wv] = rt;
-            }
-            drain_stores(); // every storing wave, before the barrier that precedes the arrival
-            __syncthreads();
-            if (threadIdx.x == 0)
-            {
-                const uint32_t it = xch[0] + xch[1] + xch[2] + xch[3];
-                st_wt(W.itot + item, it);
-                drain_stores();
-                const uint32_t old = __hip_atomic_fetch_add((gu32 *)(W.count + c), 1u, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT);
-                xch[4] = (old + 1u == citems) ? 1u : 0u;
-            }
-            __syncthreads();
-            if (xch[4] == 0u)
-                continue;
-            // ---- last arriver of chunk c: scan the item totals, chain the chunk offset
-            if (threadIdx.x == 0)
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            drain_stores();
-            __syncthreads();
-            const uint64_t i0 = static_cast<uint64_t>(c) * kPipeChunkItems;
-            const uint32_t ia = 2u * threadIdx.x, ib = ia + 1u; // kPipeChunkItems == 2 * 256
-            const uint32_t a = ia < citems ? ld_wt(W.itot + i0 + ia) : 0u;
-            const uint32_t b = ib < citems ? ld_wt(W.itot + i0 + ib) : 0u;
-            const uint32_t incl = wave_incl_scan(a + b);
-            if (t == 63)
-                xch[8 + wv] = incl;
-            __syncthreads();
-            uint32_t before = 0u;
-            for (uint32_t w = 0; w < wv; ++w)
-                before += xch[8 + w];
-            const uint32_t ex = before + incl - (a + b);
-            if (ia < citems)
-                st_wt(W.ibase + i0 + ia, ex);
-            if (ib < citems)
-                st_wt(W.ibase + i0 + ib, ex + a);
-            if (threadIdx.x == 0)
-            {
-                const uint64_t ctot = static_cast<uint64_t>(xch[8]) + xch[9] + xch[10] + xch[11];
-                uint64_t cb = 0u;
-                bool ok = true;
-                if (c > 0u)
+                if (is_plan)
                 {
-                    ok = wait_set(W.ready + (c - 1u), W.abort); // chunk c-1 is an earlier step: never circular
-                    cb = ld_wt64(W.cbase + (c - 1u)) + ld_wt64(W.ctot + (c - 1u));
+                    const uint32_t citems = static_cast<uint32_t>(min_u64(A.ci, A.nitems - static_cast<uint64_t>(c) * A.ci));
+                    pipe_plan<D1>(A, W, c, item, citems, hist[wv], xch, t, wv);
                 }
-                st_wt64(W.cbase + c, cb);
-                st_wt64(W.ctot + c, ctot);
-                if (c + 1u == nchunks)
-                    off[nblocks] = ok ? cb + ctot : ~0ull;
+                else
+                    pipe_write<D1>(A, W, c, item, img, val_all[wv], xch, t, wv);
             }
-            drain_stores();
-            __syncthreads();
-            if (threadIdx.x == 0)
-                st_wt(W.ready + c, 1u);
         }
-        else
-        {
-            // ---- write item: wait for the chunk, derive offsets, build blocks
-            // (the verdict word alternates between two LDS slots: thread 0 may
-            // write the next write item's before a slow wave has read this one)
-            const uint32_t slot = 5u + (witem++ & 1u);
-            if (threadIdx.x == 0)
-            {
-                xch[slot] = wait_set(W.ready + c, W.abort) ? 1u : 0u;
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            }
-            drain_stores();
-            __syncthreads();
-            if (xch[slot] == 0u)
-                continue;
-            if (!R.n)
-                continue;
-            uint64_t rb = ld_wt64(W.cbase + c) + ld_wt(W.ibase + item);
-            for (uint32_t w = 0; w < wv; ++w)
-                rb += ld_wt(W.rtot + item * 4u + w);
-            const uint32_t szv = t < R.n ? ld_wt(W.sz + R.first + t) : 0u;
-            const uint32_t pwv = t < R.n ? ld_wt(W.plan + R.first + t) : 0u;
-            const uint64_t ov = rb + (wave_incl_scan(szv) - szv);
-            if (t < R.n)
-                off[R.first + t] = ov;
-            write_run<D1>(R, in, starts, start0, szv, pwv, static_cast<uint32_t>(ov), static_cast<uint32_t>(ov >> 32), img,
-                          val_all[wv], out_base, cap_end, t);
-        }
+        __syncthreads(); // the prefetched ticket is visible; the item's LDS words are free again
+        q = uni(xch[nslot]);
     }
 }
 
@@ -510,12 +547,12 @@ struct PipeGeom
     size_t bytes;
 };
 
-PipeGeom pipe_geom(uint64_t nblocks)
+PipeGeom pipe_geom(uint64_t nblocks, uint32_t ci)
 {
     PipeGeom g;
     g.nitems = (nblocks + dev::kPipeItem - 1) / dev::kPipeItem;
-    g.nchunks = (g.nitems + dev::kPipeChunkItems - 1) / dev::kPipeChunkItems;
-    g.polled = ((g.nchunks * 2u + 4u) * 4u + 15u) & ~size_t(15);
+    g.nchunks = (g.nitems + ci - 1) / ci;
+    g.polled = ((8u + g.nchunks * 2u) * 4u + 15u) & ~size_t(15);
     g.bytes = al256(g.polled) + 2u * al256(g.nchunks * 8u) + 2u * al256(g.nitems * 4u) + al256(g.nitems * 16u)
               + 2u * al256(nblocks * 4u);
     return g;
@@ -525,9 +562,10 @@ dev::PipeWs pipe_ws(void * ws, uint64_t nblocks, const PipeGeom & g)
 {
     uint8_t * p = static_cast<uint8_t *>(ws);
     dev::PipeWs W;
-    W.count = reinterpret_cast<uint32_t *>(p);
+    W.head = reinterpret_cast<uint32_t *>(p);
+    W.abort = W.head + 4;
+    W.count = W.head + 8;
     W.ready = W.count + g.nchunks;
-    W.abort = W.ready + g.nchunks;
     p += al256(g.polled);
     W.cbase = reinterpret_cast<uint64_t *>(p);
     p += al256(g.nchunks * 8u);
@@ -545,40 +583,51 @@ dev::PipeWs pipe_ws(void * ws, uint64_t nblocks, const PipeGeom & g)
     return W;
 }
 
-// Workgroups of the persistent grid: every one must be resident at once
-// (the items wait on each other).  The occupancy answer can be one workgroup
-// per CU high (MI355X_MICROARCH.md, residency), so one per CU is left spare.
-template <bool D1>
+// Workgroups of the persistent grid: as many as the occupancy query admits
+// (tickets make residency a speed matter, not a correctness one).
+template <bool D1, int MINW>
 uint32_t pipe_grid(uint64_t nitems)
 {
-    static int per_cu[2][64] = {};
+    static int per_cu[2][2][64] = {};
     int dev_id = 0;
     (void)hipGetDevice(&dev_id);
     dev_id = dev_id < 0 || dev_id >= 64 ? 0 : dev_id;
-    if (per_cu[D1][dev_id] == 0)
+    int & pc = per_cu[D1][MINW == 8][dev_id];
+    if (pc == 0)
     {
         int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void *>(dev::k_enc256v32_pipe<D1>), 256, 0)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void *>(dev::k_enc256v32_pipe<D1, MINW>), 256, 0)
                 != hipSuccess
             || n <= 0)
             n = 1;
-        per_cu[D1][dev_id] = n > 1 ? n - 1 : 1;
+        pc = n;
     }
     const uint64_t want = 2u * nitems; // more workgroups than items would only idle
-    return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want, grid_cap(nullptr, per_cu[D1][dev_id]))));
+    return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want, grid_cap(nullptr, pc))));
 }
 
-template <bool D1>
+template <bool D1, int MINW>
 hipError_t launch_pipe(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, uint8_t * out, uint64_t out_cap,
-                       uint64_t * off, void * ws, hipStream_t stream)
+                       uint64_t * off, void * ws, hipStream_t stream, uint32_t ci, uint32_t lag)
 {
-    const PipeGeom g = pipe_geom(nblocks);
+    const PipeGeom g = pipe_geom(nblocks, ci);
     const dev::PipeWs W = pipe_ws(ws, nblocks, g);
-    hipError_t e = hipMemsetAsync(W.count, 0, g.polled, stream);
+    hipError_t e = hipMemsetAsync(W.head, 0, g.polled, stream);
     if (e != hipSuccess)
         return e;
-    hipLaunchKernelGGL(dev::k_enc256v32_pipe<D1>, dim3(pipe_grid<D1>(g.nitems)), dim3(256), 0, stream, in, nblocks, starts,
-                       start0, out, out_cap, off, W, static_cast<uint32_t>(g.nchunks), g.nitems);
+    dev::PipeArgs A;
+    A.in = in;
+    A.nblocks = nblocks;
+    A.starts = starts;
+    A.start0 = start0;
+    A.out_base = reinterpret_cast<uint64_t>(out);
+    A.cap_end = A.out_base + out_cap;
+    A.off = off;
+    A.nitems = g.nitems;
+    A.nchunks = static_cast<uint32_t>(g.nchunks);
+    A.ci = ci;
+    A.lag = lag;
+    hipLaunchKernelGGL((dev::k_enc256v32_pipe<D1, MINW>), dim3(pipe_grid<D1, MINW>(g.nitems)), dim3(256), 0, stream, A, W);
     e = hipGetLastError();
     if (e != hipSuccess)
         return e;
@@ -586,9 +635,18 @@ hipError_t launch_pipe(const uint32_t * in, uint64_t nblocks, const uint32_t * s
     return hipGetLastError();
 }
 
+template <bool D1>
+hipError_t launch_pipe_w(int minw, const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, uint8_t * out,
+                         uint64_t out_cap, uint64_t * off, void * ws, hipStream_t stream, uint32_t ci, uint32_t lag)
+{
+    return minw == 7 ? launch_pipe<D1, 7>(in, nblocks, starts, start0, out, out_cap, off, ws, stream, ci, lag)
+                     : launch_pipe<D1, 8>(in, nblocks, starts, start0, out, out_cap, off, ws, stream, ci, lag);
+}
+
 } // namespace
 
-size_t enc256v32_workspace(uint64_t nblocks) { return std::max(twopass_workspace(nblocks), pipe_geom(nblocks).bytes); }
+// the pipelined encoder's workspace is largest at the smallest chunk it may run with (64 items)
+size_t enc256v32_workspace(uint64_t nblocks) { return std::max(twopass_workspace(nblocks), pipe_geom(nblocks, 64).bytes); }
 
 hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, bool d1,
                             uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t stream,
@@ -598,9 +656,16 @@ hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_
         return hipMemsetAsync(off, 0, sizeof(uint64_t), stream);
     if (nblocks + 1 > 0x7FFFFFFFull)
         return hipErrorInvalidValue;
-    if (probe == 0)
-        return d1 ? launch_pipe<true>(in, nblocks, starts, start0, out, out_cap, off, ws, stream)
-                  : launch_pipe<false>(in, nblocks, starts, start0, out, out_cap, off, ws, stream);
+    if (probe == 0 || probe >= 16)
+    {
+        // probe >= 16 (measurement): 16 + ci + 1024 * lag + 65536 * (7 minimum waves per SIMD instead of 8)
+        const uint32_t ci = probe >= 16 ? std::min<uint32_t>(dev::kPipeMaxChunkItems, std::max<uint32_t>(64, (probe - 16) % 1024))
+                                        : dev::kPipeChunkItems;
+        const uint32_t lag = probe >= 16 ? std::max<uint32_t>(1, (static_cast<uint32_t>(probe - 16) / 1024) % 64) : dev::kPipeLag;
+        const int minw = probe >= 16 && ((probe - 16) >> 16) ? 7 : dev::kPipeMinWaves;
+        return d1 ? launch_pipe_w<true>(minw, in, nblocks, starts, start0, out, out_cap, off, ws, stream, ci, lag)
+                  : launch_pipe_w<false>(minw, in, nblocks, starts, start0, out, out_cap, off, ws, stream, ci, lag);
+    }
     // probe 1 / 2: the two-pass passes with the coding removed; 3: the two-pass encoder itself (A/B)
     uint32_t * plan = static_cast<uint32_t *>(ws);
     const size_t plan_bytes = al256(nblocks * 4u);
