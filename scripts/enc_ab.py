@@ -37,10 +37,15 @@ def probe(mode):
 
 
 twopass = probe(3)
-# pipelined variants: 16 + chunk items + 1024 * lag + 65536 * (7 waves/SIMD bound)
+# pipelined variants: 16 + chunk items + 1024 * lag + 65536 * minw + 2^20 * entries per ticket
+def pv(ci, lag, minw, k):
+    return probe(16 + ci + 1024 * lag + 65536 * minw + (1 << 20) * k)
+
+
 VARIANTS = [("twopass", twopass), ("pipe", pipe)] + [
-    (f"ci{ci}_lag{lag}_w{w}", probe(16 + ci + 1024 * lag + 65536 * (w == 7)))
-    for ci, lag, w in [(256, 1, 8), (256, 3, 8), (128, 2, 8), (128, 4, 8), (512, 1, 8), (256, 2, 7)]]
+    (f"ci{ci}_lag{lag}_w{w}_k{k}", pv(ci, lag, w, k))
+    for ci, lag, w, k in [(256, 2, 8, 8), (256, 2, 0, 8), (256, 2, 6, 8), (256, 2, 8, 16), (256, 4, 8, 8),
+                          (512, 2, 0, 8), (128, 4, 0, 8)]]
 
 
 def timed(fn, reps=10):

@@ -284,6 +284,7 @@ constexpr uint32_t kPipeMaxChunkItems = 512; // the last arriver's scan covers 2
 constexpr uint32_t kPipeChunkItems = 256;    // default: 32K blocks = 32 MiB of values per chunk
 constexpr uint32_t kPipeLag = 2;             // default: chunk c is written in step c + 2
 constexpr int kPipeMinWaves = 8;             // default launch bound: 8 waves per SIMD
+constexpr uint32_t kPipePerTicket = 8;       // default: sequence entries per ticket
 constexpr uint32_t kSpinLimit = 1u << 22;    // polls of ~0.2 us
 
 typedef __attribute__((address_space(1))) uint32_t gu32;
@@ -352,7 +353,7 @@ struct PipeArgs
     uint64_t out_base, cap_end;
     uint64_t * off;
     uint64_t nitems;
-    uint32_t nchunks, ci, lag;
+    uint32_t nchunks, ci, lag, per_ticket;
 };
 
 // Plan item: plan 4 runs of kPipeRun blocks, publish sizes / plan words / run
@@ -476,20 +477,20 @@ __global__ __launch_bounds__(256, MINW) void k_enc256v32_pipe(PipeArgs A, PipeWs
     zero_image(img, kImgU32 / 4u, t);
     wave_lds_sync();
     const uint32_t nseq = (A.nchunks + A.lag) * (2u * A.ci);
-    // Items come from a ticket counter, in sequence order, and every
-    // workgroup runs its tickets in order: a write item then waits only on
-    // plan items that running workgroups hold, so there is no residency
-    // assumption (a static item -> workgroup map would need every workgroup
-    // resident).  The next ticket is taken while the current item runs.
+    // Items come from a ticket counter, A.per_ticket consecutive sequence
+    // entries per ticket, and every workgroup runs its entries in order: a
+    // write item then waits only on plan items that running workgroups hold,
+    // so there is no residency assumption (a static item -> workgroup map
+    // would need every workgroup resident).  The next ticket is taken by the
+    // last wave after its share of the last entry of the current one, so its
+    // latency (one contended word) sits behind that wave's work only.
     if (threadIdx.x == 0)
-        xch[12] = __hip_atomic_fetch_add((gu32 *)W.head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        xch[12] = __hip_atomic_fetch_add((gu32 *)W.head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * A.per_ticket;
     __syncthreads();
     uint32_t q = xch[12];
-    for (uint32_t it = 0; q < nseq; ++it)
+    while (q < nseq)
     {
-        const uint32_t nslot = 12u + ((it + 1u) & 1u);
-        if (threadIdx.x == 0)
-            xch[nslot] = __hip_atomic_fetch_add((gu32 *)W.head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last_of_ticket = (q + 1u) % A.per_ticket == 0u;
         // sequence: step s = plan items of chunk s interleaved with write items of chunk s - lag
         const uint32_t step = q / (2u * A.ci);
         const uint32_t r = q % (2u * A.ci);
@@ -509,8 +510,18 @@ __global__ __launch_bounds__(256, MINW) void k_enc256v32_pipe(PipeArgs A, PipeWs
                     pipe_write<D1>(A, W, c, item, img, val_all[wv], xch, t, wv);
             }
         }
-        __syncthreads(); // the prefetched ticket is visible; the item's LDS words are free again
-        q = uni(xch[nslot]);
+        if (last_of_ticket)
+        {
+            if (threadIdx.x == 192)
+                xch[12] = __hip_atomic_fetch_add((gu32 *)W.head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * A.per_ticket;
+            __syncthreads(); // the new ticket is visible; the item's LDS words are free again
+            q = uni(xch[12]);
+        }
+        else
+        {
+            __syncthreads(); // the item's LDS words are free again
+            ++q;
+        }
     }
 }
 
@@ -588,11 +599,11 @@ dev::PipeWs pipe_ws(void * ws, uint64_t nblocks, const PipeGeom & g)
 template <bool D1, int MINW>
 uint32_t pipe_grid(uint64_t nitems)
 {
-    static int per_cu[2][2][64] = {};
+    static int per_cu[2][3][64] = {};
     int dev_id = 0;
     (void)hipGetDevice(&dev_id);
     dev_id = dev_id < 0 || dev_id >= 64 ? 0 : dev_id;
-    int & pc = per_cu[D1][MINW == 8][dev_id];
+    int & pc = per_cu[D1][MINW == 8 ? 0 : MINW == 6 ? 1 : 2][dev_id];
     if (pc == 0)
     {
         int n = 0;
@@ -608,7 +619,7 @@ uint32_t pipe_grid(uint64_t nitems)
 
 template <bool D1, int MINW>
 hipError_t launch_pipe(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, uint8_t * out, uint64_t out_cap,
-                       uint64_t * off, void * ws, hipStream_t stream, uint32_t ci, uint32_t lag)
+                       uint64_t * off, void * ws, hipStream_t stream, uint32_t ci, uint32_t lag, uint32_t per_ticket)
 {
     const PipeGeom g = pipe_geom(nblocks, ci);
     const dev::PipeWs W = pipe_ws(ws, nblocks, g);
@@ -627,6 +638,7 @@ hipError_t launch_pipe(const uint32_t * in, uint64_t nblocks, const uint32_t * s
     A.nchunks = static_cast<uint32_t>(g.nchunks);
     A.ci = ci;
     A.lag = lag;
+    A.per_ticket = per_ticket;
     hipLaunchKernelGGL((dev::k_enc256v32_pipe<D1, MINW>), dim3(pipe_grid<D1, MINW>(g.nitems)), dim3(256), 0, stream, A, W);
     e = hipGetLastError();
     if (e != hipSuccess)
@@ -637,10 +649,18 @@ hipError_t launch_pipe(const uint32_t * in, uint64_t nblocks, const uint32_t * s
 
 template <bool D1>
 hipError_t launch_pipe_w(int minw, const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, uint8_t * out,
-                         uint64_t out_cap, uint64_t * off, void * ws, hipStream_t stream, uint32_t ci, uint32_t lag)
+                         uint64_t out_cap, uint64_t * off, void * ws, hipStream_t stream, uint32_t ci, uint32_t lag,
+                         uint32_t per_ticket)
 {
-    return minw == 7 ? launch_pipe<D1, 7>(in, nblocks, starts, start0, out, out_cap, off, ws, stream, ci, lag)
-                     : launch_pipe<D1, 8>(in, nblocks, starts, start0, out, out_cap, off, ws, stream, ci, lag);
+    switch (minw)
+    {
+        case 8:
+            return launch_pipe<D1, 8>(in, nblocks, starts, start0, out, out_cap, off, ws, stream, ci, lag, per_ticket);
+        case 6:
+            return launch_pipe<D1, 6>(in, nblocks, starts, start0, out, out_cap, off, ws, stream, ci, lag, per_ticket);
+        default:
+            return launch_pipe<D1, 1>(in, nblocks, starts, start0, out, out_cap, off, ws, stream, ci, lag, per_ticket);
+    }
 }
 
 } // namespace
@@ -658,13 +678,16 @@ hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_
         return hipErrorInvalidValue;
     if (probe == 0 || probe >= 16)
     {
-        // probe >= 16 (measurement): 16 + ci + 1024 * lag + 65536 * (7 minimum waves per SIMD instead of 8)
-        const uint32_t ci = probe >= 16 ? std::min<uint32_t>(dev::kPipeMaxChunkItems, std::max<uint32_t>(64, (probe - 16) % 1024))
+        // probe >= 16 (measurement): 16 + ci + 1024 * lag + 65536 * minw + 2^20 * per_ticket
+        // (minw: launch bound in waves per SIMD, 8 / 6 / other = none)
+        const uint32_t pv = static_cast<uint32_t>(probe - 16);
+        const uint32_t ci = probe >= 16 ? std::min<uint32_t>(dev::kPipeMaxChunkItems, std::max<uint32_t>(64, pv % 1024))
                                         : dev::kPipeChunkItems;
-        const uint32_t lag = probe >= 16 ? std::max<uint32_t>(1, (static_cast<uint32_t>(probe - 16) / 1024) % 64) : dev::kPipeLag;
-        const int minw = probe >= 16 && ((probe - 16) >> 16) ? 7 : dev::kPipeMinWaves;
-        return d1 ? launch_pipe_w<true>(minw, in, nblocks, starts, start0, out, out_cap, off, ws, stream, ci, lag)
-                  : launch_pipe_w<false>(minw, in, nblocks, starts, start0, out, out_cap, off, ws, stream, ci, lag);
+        const uint32_t lag = probe >= 16 ? std::max<uint32_t>(1, (pv / 1024) % 64) : dev::kPipeLag;
+        const int minw = probe >= 16 ? static_cast<int>((pv >> 16) & 15u) : dev::kPipeMinWaves;
+        const uint32_t per_ticket = probe >= 16 ? std::max<uint32_t>(1, pv >> 20) : dev::kPipePerTicket;
+        return d1 ? launch_pipe_w<true>(minw, in, nblocks, starts, start0, out, out_cap, off, ws, stream, ci, lag, per_ticket)
+                  : launch_pipe_w<false>(minw, in, nblocks, starts, start0, out, out_cap, off, ws, stream, ci, lag, per_ticket);
     }
     // probe 1 / 2: the two-pass passes with the coding removed; 3: the two-pass encoder itself (A/B)
     uint32_t * plan = static_cast<uint32_t *>(ws);
