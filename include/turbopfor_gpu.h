@@ -95,10 +95,7 @@ int tpf_p4d1dec256v32_chain_decode(const uint8_t *d_in, uint64_t in_bytes, const
  * d_ws: device workspace of tpf_p4enc256v32_workspace_size(nblocks) bytes.
  * D1: d_starts[i] is the value preceding block i; with d_starts == NULL the
  * blocks are one chained posting list: block 0 starts from start0 and block
- * i>0 from the last input value of block i-1.
- * One persistent launch (p4_enc256v32.hip): if its workgroups cannot all be
- * resident (the device held by other work for over ~1 s), it gives up and
- * stores UINT64_MAX in d_off[nblocks] instead of hanging. */
+ * i>0 from the last input value of block i-1. */
 uint64_t tpf_p4enc256v32_bound(uint64_t nblocks);
 size_t tpf_p4enc256v32_workspace_size(uint64_t nblocks);
 int tpf_p4enc256v32_batch(const uint32_t *d_in, uint64_t nblocks, uint8_t *d_out, uint64_t out_cap, uint64_t *d_off,
@@ -108,8 +105,10 @@ int tpf_p4d1enc256v32_batch(const uint32_t *d_in, uint64_t nblocks, const uint32
 /* Measurement only (no reference counterpart): mode 1 = the two-pass
  * encoder's plan pass reduced to a wave OR, 2 = its write pass copying the
  * staged values (same loads and stores, output NOT a valid stream); 3 = the
- * two-pass encoder itself (plan, offset scan, write: a valid stream), kept
- * for A/B against the production single-launch encoder.  Arguments as
+ * production two-pass encoder (= tpf_p4enc256v32_batch); >= 16 = the rejected
+ * single-launch pipelined encoder (a valid stream; 16 + chunk items + 1024 *
+ * lag + 65536 * launch-bound waves + 2^20 * entries per ticket, DESIGN.md
+ * 4.4; UINT64_MAX in d_off[nblocks] if a bounded wait expired).  Arguments as
  * tpf_p4enc256v32_batch. */
 int tpf_probe_enc256v32(int mode, const uint32_t *d_in, uint64_t nblocks, uint8_t *d_out, uint64_t out_cap,
                         uint64_t *d_off, void *d_ws, size_t ws_bytes, void *stream);

@@ -196,7 +196,7 @@ __device__ __forceinline__ void write_run(const EncRun & R, const uint32_t * in,
     });
 }
 
-// ---- two-pass encoder (plan -> hipcub scan -> write): kept for A/B ---------
+// ---- two-pass encoder (plan -> hipcub scan -> write): the production path ---
 template <bool D1, int PROBE = 0>
 __global__ __launch_bounds__(256) void k_enc256v32_plan(const uint32_t * __restrict in, uint64_t nblocks,
                                                          const uint32_t * __restrict starts, uint32_t start0,
@@ -245,39 +245,41 @@ __global__ __launch_bounds__(256) void k_enc256v32_write(const uint32_t * __rest
                          val_all[wv], out_base, out_base + out_cap, t);
 }
 
-// ---- single-launch pipelined encoder ---------------------------------------
-// The blocks are cut into chunks of kPipeChunkItems workgroup items of
-// kPipeItem blocks (4 waves x kPipeRun).  ONE persistent launch walks a fixed
-// sequence of items, step s = [plan items of chunk s] interleaved with
-// [write items of chunk s - 1]:
-//   plan item  : plans its 128 blocks (p4Bits32 cost model), publishes each
-//                block's size and plan word, its runs' and its own byte
-//                totals, and arrives on the chunk's counter; the LAST arriving
-//                item scans the chunk's item totals (item offsets inside the
+// ---- single-launch pipelined encoder: MEASURED AND REJECTED ---
+// Reachable only through tpf_probe_enc256v32 (mode >= 16).  Every variant is
+// byte-exact, and none is faster than the two-pass encoder above.
+// The blocks are cut into chunks of `ci` workgroup items of kPipeItem blocks
+// (4 waves x kPipeRun).  ONE persistent launch walks a sequence of items,
+// step s = plan items of chunk s interleaved with write items of chunk
+// s - lag:
+//   plan item  : plans its blocks (p4Bits32 cost model), publishes each
+//                block's size and plan word and its run / item byte totals,
+//                and arrives on the chunk's counter; the LAST arriving item
+//                scans the chunk's item totals (item offsets inside the
 //                chunk), chains the chunk's byte offset from the previous
 //                chunk's and flags the chunk ready;
 //   write item : waits for its chunk's flag, derives every block's byte
-//                offset (chunk offset + item offset + run offset + in-run scan),
-//                writes d_off and builds the blocks exactly as the two-pass
-//                write kernel does.
-// A chunk's values (64 MiB) are re-read by its write items one step after its
-// plan items read them, while the 256 MiB Infinity Cache still holds them, so
-// the second read costs no HBM traffic (the two-pass encoder re-reads all
-// values from HBM: 1.33x algorithmic traffic, profiles/pmc_traffic.json c4),
-// the offset scan needs no extra launch, and the compute-heavy planning of
-// one chunk runs beside the memory-heavy writing of the previous one.
+//                offset (chunk + item + run offset + in-run scan), writes
+//                d_off and builds the blocks as the two-pass write kernel does.
+// The aim: a chunk's values are re-read by its write items while the 256 MiB
+// Infinity Cache still holds them (no second HBM read: the two-pass encoder
+// moves 1.33x the algorithmic bytes), no separate scan launch, planning of one
+// chunk beside writing of an earlier one.  Why it loses: a write item cannot
+// start before EVERY plan item of its chunk and the chunk chain before it are
+// done, while the machine keeps G x kPipeItem blocks (~160 MB of values at
+// 1280-2048 workgroups) in flight; a lag that hides that window no longer
+// fits the Infinity Cache with the chunks it needs, and any shorter lag makes
+// the write items wait (measured 8.3 ms with a static item map, 19-79 ms with
+// tickets, vs 5.45 ms two-pass, C4 mix, 10M blocks).
 // Hand-offs (MI355X_MICROARCH.md "visibility", cdna_hip_programming.md G16):
 // every published word is stored write-through (agent-scope relaxed atomic
 // store = sc1) and drained (s_waitcnt vmcnt(0)) by every storing wave before
 // the workgroup barrier and the counter add / flag store; consumers poll one
-// word relaxed with s_sleep, take ONE agent-scope acquire and read the
-// published words with sc1 loads.  Deadlock-free with every workgroup
-// resident (grid sized from the occupancy query, one workgroup per CU
-// spare): a write item waits only for plan items of an EARLIER step and the
-// last arriver of chunk c only for chunk c-1's flag, so the earliest
-// unfinished item of the sequence can always proceed.  Every wait is bounded
-// (kSpinLimit polls): on expiry the kernel raises an abort word and a finish
-// kernel stores UINT64_MAX in d_off[nblocks].
+// word relaxed with s_sleep, take ONE agent-scope acquire and read the words
+// with sc1 loads.  Items come from a ticket counter in sequence order (no
+// residency assumption, see the kernel); every wait is bounded (kSpinLimit
+// polls): on expiry the kernel raises an abort word and a finish kernel
+// stores UINT64_MAX in d_off[nblocks].
 constexpr uint32_t kPipeRun = 32;
 constexpr uint32_t kPipeItem = 4u * kPipeRun;
 constexpr uint32_t kPipeMaxChunkItems = 512; // the last arriver's scan covers 2 items per thread
@@ -676,7 +678,7 @@ hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_
         return hipMemsetAsync(off, 0, sizeof(uint64_t), stream);
     if (nblocks + 1 > 0x7FFFFFFFull)
         return hipErrorInvalidValue;
-    if (probe == 0 || probe >= 16)
+    if (probe >= 16)
     {
         // probe >= 16 (measurement): 16 + ci + 1024 * lag + 65536 * minw + 2^20 * per_ticket
         // (minw: launch bound in waves per SIMD, 8 / 6 / other = none)
@@ -689,7 +691,7 @@ hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_
         return d1 ? launch_pipe_w<true>(minw, in, nblocks, starts, start0, out, out_cap, off, ws, stream, ci, lag, per_ticket)
                   : launch_pipe_w<false>(minw, in, nblocks, starts, start0, out, out_cap, off, ws, stream, ci, lag, per_ticket);
     }
-    // probe 1 / 2: the two-pass passes with the coding removed; 3: the two-pass encoder itself (A/B)
+    // the production two-pass encoder (probe 0 / 3), or its passes with the coding removed (probe 1 / 2)
     uint32_t * plan = static_cast<uint32_t *>(ws);
     const size_t plan_bytes = al256(nblocks * 4u);
     void * scan_tmp = static_cast<uint8_t *>(ws) + plan_bytes;
