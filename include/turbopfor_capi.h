@@ -52,6 +52,14 @@ unsigned char *tpf_p4D1Enc256v64(uint64_t *in, unsigned n, unsigned char *out, u
 const unsigned char *tpf_p4Dec256v64(const unsigned char *in, unsigned n, uint64_t *out);
 const unsigned char *tpf_p4D1Dec256v64(const unsigned char *in, unsigned n, uint64_t *out, uint64_t start);
 
+/* How the per-block calls above reach the GPU (identical bytes either way):
+ * 0 (default) = a resident block server kernel polling mailboxes in coherent
+ * pinned host memory (no launch per call; it exits after 10 ms without
+ * calls and is relaunched on the next one), 1 = one batched launch plus a
+ * stream synchronise per call.  mode < 0 only queries.  Returns the
+ * previous mode. */
+int tpf_perblock_mode(int mode);
+
 /* ---- stream framing (host, no decoding) -------------------
  * Encoded length of the block at `in` (fmt = TPF_FMT_*, n = values per call),
  * reading at most `avail` bytes; 0 if malformed/truncated.  values_written

@@ -27,9 +27,21 @@ def capi():
     return L
 
 
+@pytest.fixture(params=[0, 1], ids=["server", "launch"])
+def perblock_mode(request):
+    """Both per-block designs (tpf_perblock_mode): the resident block server
+    (default) and one launch + synchronise per call."""
+    L = capi()
+    L.tpf_perblock_mode.restype = ctypes.c_int
+    L.tpf_perblock_mode.argtypes = [ctypes.c_int]
+    prev = L.tpf_perblock_mode(request.param)
+    yield request.param
+    L.tpf_perblock_mode(prev)
+
+
 @pytest.mark.parametrize("fname,fmt", [("g32.bin", "32"), ("g128v32.bin", "128v32"), ("g256v32.bin", "256v32"),
                                        ("g128v64.bin", "128v64"), ("g256v64.bin", "256v64")])
-def test_per_block_mirrors_match_golden(fname, fmt):
+def test_per_block_mirrors_match_golden(fname, fmt, perblock_mode):
     L = capi()
     wide = fmt in ("128v64", "256v64")
     dt = np.uint64 if wide else np.uint32
@@ -225,4 +237,43 @@ def test_host_streams_concurrent_threads(monkeypatch):
         th.start()
     for th in threads:
         th.join()
+    assert not errors, errors
+
+
+def test_per_block_server_concurrent_threads():
+    """Eight threads share the block server's four mailboxes: every thread's
+    encode -> decode round trip of its own blocks is byte-exact (oracle) and
+    bit-exact."""
+    import threading
+
+    L = capi()
+    L.tpf_p4Enc256v32.restype = ctypes.c_void_p
+    L.tpf_p4Enc256v32.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]
+    L.tpf_p4D1Dec256v32.restype = ctypes.c_void_p
+    L.tpf_p4D1Dec256v32.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p, ctypes.c_uint32]
+    L.tpf_p4Dec256v32.restype = ctypes.c_void_p
+    L.tpf_p4Dec256v32.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]
+    errors = []
+
+    def worker(k):
+        try:
+            blocks = datagen.c2_blocks(60, 3 + 3 * k, 10, seed=k)
+            for v in blocks:
+                v = np.ascontiguousarray(v)
+                buf = np.zeros(4096, np.uint8)
+                end = L.tpf_p4Enc256v32(v.ctypes.data, 256, buf.ctypes.data)
+                assert end is not None
+                enc = bytes(buf[: end - buf.ctypes.data])
+                assert enc == oracle_lib.encode("256v32", v)
+                out = np.zeros(256, np.uint32)
+                assert L.tpf_p4Dec256v32(buf.ctypes.data, 256, out.ctypes.data) == end
+                assert np.array_equal(out, v)
+        except Exception as e:  # noqa: BLE001
+            errors.append((k, repr(e)))
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
     assert not errors, errors

@@ -1,23 +1,30 @@
 // host_api.cpp -- the drop-in boundary: include/turbopfor.h (C++ linkage,
 // signature-identical to the reference's include/turbopfor.h:9-80), its
 // extern "C" mirror include/turbopfor_capi.h, and the host-memory stream
-// entry points.  Every call runs the gfx950 kernels through the batched
-// C-ABI (capi.cpp); nothing here encodes or decodes a value on the CPU.
+// entry points.  Every call runs the gfx950 kernels; nothing here encodes or
+// decodes a value on the CPU.
 //
-// Per-block calls keep a thread-local context (HIP stream, pinned staging,
-// device workspace) on the thread's current device: copy one block's values
-// or bytes into pinned staging, launch with nblocks = 1 on the staging's
-// device addresses (zero-copy over PCIe), synchronise.  That is
-// latency-bound (18 us per p4Dec256v32 call, 24 us per p4Enc256v32 on MI355X:
-// the launch and its completion, not the copies) and exists so that a
-// reference caller relinks and gets identical bytes; throughput callers use
-// tpf_host_dec/tpf_host_enc (pipelined host streams) or turbopfor_gpu.h
-// (device-resident batches).
+// Per-block calls (one block per call, as reference callers chain them) go
+// to the resident block server (p4_server.hip, tpf_server.h): the call
+// copies the block into a mailbox in coherent pinned host memory, bumps the
+// request word and spins until the kernel acknowledges -- no launch, no
+// stream synchronise per call.  tpf_perblock_mode(1) selects the first
+// design instead (a thread-local stream and pinned staging, one batched
+// launch with nblocks = 1 on the staging's device addresses, synchronise:
+// 18-24 us per call, the launch + synchronise floor).  Both give identical
+// bytes; throughput callers use tpf_host_dec/tpf_host_enc (pipelined host
+// streams) or turbopfor_gpu.h (device-resident batches).
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -25,6 +32,8 @@
 #include "../../include/turbopfor.h"
 #include "../../include/turbopfor_capi.h"
 #include "../../include/turbopfor_gpu.h"
+#include "tpf_kernels.h"
+#include "tpf_server.h"
 
 namespace
 {
@@ -153,6 +162,198 @@ struct Ctx
     ~Ctx() { reset(); }
 };
 
+// ---- resident block server (per device) ------------------------------------
+std::atomic<int> g_mode{0}; // 0 = block server, 1 = launch + synchronise per call
+
+struct Server
+{
+    int dev = -1;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr; // recorded after the current launch
+    bool launched = false;
+    tpf::ServerCtl * h = nullptr; // coherent pinned mailboxes (host view)
+    tpf::ServerCtl * d = nullptr; // the same memory, device view
+    std::mutex mu;                // launches, event queries, mailbox leases
+    std::condition_variable cv;
+    uint32_t free_mask = (1u << tpf::kServerBoxes) - 1u;
+    uint32_t reqno[tpf::kServerBoxes] = {};
+
+    explicit Server(int device) : dev(device)
+    {
+        hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "server stream");
+        hip_check(hipEventCreateWithFlags(&done, hipEventDisableTiming), "server event");
+        void * p = nullptr;
+        hip_check(hipHostMalloc(&p, sizeof(tpf::ServerCtl), hipHostMallocCoherent | hipHostMallocPortable), "mailboxes");
+        std::memset(p, 0, sizeof(tpf::ServerCtl));
+        h = static_cast<tpf::ServerCtl *>(p);
+        void * dp = nullptr;
+        hip_check(hipHostGetDevicePointer(&dp, p, 0), "mailbox device address");
+        d = static_cast<tpf::ServerCtl *>(dp);
+    }
+
+    // caller holds mu
+    void launch()
+    {
+        hip_check(tpf::launch_block_server(d, stream), "block server launch");
+        hip_check(hipEventRecord(done, stream), "block server event");
+        launched = true;
+    }
+    // caller holds mu: has the current launch ended (idle exit or stop)?
+    bool ended()
+    {
+        if (!launched)
+            return true;
+        const hipError_t e = hipEventQuery(done);
+        if (e == hipErrorNotReady)
+            return false;
+        hip_check(e, "block server");
+        return true;
+    }
+
+    int lease()
+    {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return free_mask != 0u; });
+        const int i = __builtin_ctz(free_mask);
+        free_mask &= ~(1u << i);
+        return i;
+    }
+    void release(int i)
+    {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            free_mask |= 1u << i;
+        }
+        cv.notify_one();
+    }
+
+    // Post the request prepared in mailbox i and wait for its acknowledgement.
+    void call(int i)
+    {
+        tpf::ServerBox * b = &h->box[i];
+        const uint32_t r = ++reqno[i];
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (ended())
+                launch();
+        }
+        std::atomic_thread_fence(std::memory_order_release);
+        __atomic_store_n(&b->req, r, __ATOMIC_RELEASE);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint64_t spin = 1;; ++spin)
+        {
+            if (__atomic_load_n(&b->ack, __ATOMIC_ACQUIRE) == r)
+                break;
+            _mm_pause();
+            if ((spin & 1023u) == 0u)
+            {
+                // the launch may have idled out just before this request: relaunch
+                std::lock_guard<std::mutex> g(mu);
+                if (ended() && __atomic_load_n(&b->ack, __ATOMIC_ACQUIRE) != r)
+                    launch();
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20))
+                    throw std::runtime_error("turbopfor_amd: block server did not answer within 20 s");
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    }
+
+    void stop()
+    {
+        std::lock_guard<std::mutex> g(mu);
+        __atomic_store_n(&h->stop, 1u, __ATOMIC_RELEASE);
+        if (launched)
+            (void)hipEventSynchronize(done);
+        __atomic_store_n(&h->stop, 0u, __ATOMIC_RELEASE);
+    }
+};
+
+std::mutex g_srv_mu;
+Server * g_srv[64] = {};
+
+void stop_servers()
+{
+    std::lock_guard<std::mutex> g(g_srv_mu);
+    for (Server * s : g_srv)
+        if (s)
+            s->stop();
+}
+
+Server & server()
+{
+    int dev = 0;
+    hip_check(hipGetDevice(&dev), "hipGetDevice");
+    if (dev < 0 || dev >= 64)
+        throw std::runtime_error("turbopfor_amd: device index out of range");
+    std::lock_guard<std::mutex> g(g_srv_mu);
+    if (!g_srv[dev])
+    {
+        static bool registered = false;
+        if (!registered)
+        {
+            std::atexit(stop_servers); // before HIP's own teardown (registered earlier, runs later)
+            registered = true;
+        }
+        g_srv[dev] = new Server(dev);
+    }
+    return *g_srv[dev];
+}
+
+struct BoxLease
+{
+    Server & s;
+    int i;
+    explicit BoxLease(Server & srv) : s(srv), i(srv.lease()) { }
+    ~BoxLease() { s.release(i); }
+    tpf::ServerBox * box() const { return &s.h->box[i]; }
+};
+
+unsigned char * enc_srv(int fmt, const void * in, unsigned n, unsigned char * out, bool d1, uint64_t start)
+{
+    Server & S = server();
+    BoxLease L(S);
+    tpf::ServerBox * b = L.box();
+    const size_t es = wide_fmt(fmt) ? 8 : 4;
+    const size_t vbytes = es * unit_values(fmt, n); // the reference also reads the full block width
+    std::memcpy(b->in, in, vbytes);
+    b->op = tpf::kOpEnc;
+    b->fmt = static_cast<uint32_t>(fmt);
+    b->n = n;
+    b->d1 = d1 ? 1u : 0u;
+    b->start = start;
+    b->in_len = static_cast<uint32_t>(vbytes);
+    S.call(L.i);
+    const uint32_t size = b->result;
+    if (size == 0xFFFFFFFFu || size > tpf::kServerPayload)
+        throw std::runtime_error("turbopfor_amd: block server rejected the encode request");
+    std::memcpy(out, b->out, size);
+    return out + size;
+}
+
+const unsigned char * dec_srv(int fmt, const unsigned char * in, unsigned n, void * out, bool d1, uint64_t start)
+{
+    int written = 0;
+    const uint64_t size = tpf_block_size(fmt, in, uint64_t(1) << 20, n, &written);
+    if (size == 0 || size > tpf::kServerPayload)
+        throw std::runtime_error("turbopfor_amd: malformed P4 block header");
+    Server & S = server();
+    BoxLease L(S);
+    tpf::ServerBox * b = L.box();
+    std::memcpy(b->in, in, size);
+    b->op = tpf::kOpDec;
+    b->fmt = static_cast<uint32_t>(fmt);
+    b->n = n;
+    b->d1 = d1 ? 1u : 0u;
+    b->start = start;
+    b->in_len = static_cast<uint32_t>(size);
+    S.call(L.i);
+    if (b->result != size)
+        throw std::runtime_error("turbopfor_amd: malformed P4 block (length check failed on the device)");
+    const size_t es = wide_fmt(fmt) ? 8 : 4;
+    std::memcpy(out, b->out, es * b->written);
+    return in + size;
+}
+
 // One-block encode through tpf_enc_batch.  Zero-copy: the kernels read the
 // values from, and write the bytes and offsets to, pinned host staging, so a
 // call is one launch sequence and one synchronise (the first version staged
@@ -161,6 +362,8 @@ unsigned char * enc_one(int fmt, const void * in, unsigned n, unsigned char * ou
 {
     if (n == 0)
         return out;
+    if (g_mode.load(std::memory_order_relaxed) == 0)
+        return enc_srv(fmt, in, n, out, d1, start);
     Ctx & c = Ctx::get();
     const size_t es = wide_fmt(fmt) ? 8 : 4;
     const size_t vbytes = es * unit_values(fmt, n);
@@ -186,6 +389,8 @@ const unsigned char * dec_one(int fmt, const unsigned char * in, unsigned n, voi
 {
     if (n == 0)
         return in;
+    if (g_mode.load(std::memory_order_relaxed) == 0)
+        return dec_srv(fmt, in, n, out, d1, start);
     Ctx & c = Ctx::get();
     int written = 0;
     // the block's length comes from its own header (framing.cpp); 1 MiB is far
@@ -341,6 +546,11 @@ const unsigned char * p4D1Dec256v64(const unsigned char * in, unsigned n, uint64
 
 // ----------------------------------------------------------- extern "C" mirror
 extern "C" {
+
+int tpf_perblock_mode(int mode)
+{
+    return mode >= 0 ? g_mode.exchange(mode == 1 ? 1 : 0) : g_mode.load();
+}
 
 #define TPF_MIRROR_ENC(NAME, T)                                                                                  \
     unsigned char * tpf_##NAME(T * in, unsigned n, unsigned char * out)                                          \

@@ -337,6 +337,36 @@ __device__ __forceinline__ T delta1_g(T v[4], uint32_t n, T start, uint32_t t)
     return carry;
 }
 
+// deltaEnc1 (p4_scalar_internal.h:711-719) over elements e < n in order.
+template <class T>
+__device__ __forceinline__ void delta_enc_g(T v[4], T prev0, uint32_t n, uint32_t t)
+{
+    T d[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j)
+    {
+        T prev;
+        if constexpr (sizeof(T) == 8)
+        {
+            const uint32_t lo = static_cast<uint32_t>(__shfl_up(static_cast<int>(static_cast<uint32_t>(v[j])), 1, 64));
+            const uint32_t hi = static_cast<uint32_t>(__shfl_up(static_cast<int>(static_cast<uint32_t>(v[j] >> 32)), 1, 64));
+            prev = (static_cast<uint64_t>(hi) << 32) | lo;
+            if (t == 0)
+                prev = j == 0 ? prev0 : readlane_u64(v[j - 1], 63);
+        }
+        else
+        {
+            prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(v[j]), 1, 64));
+            if (t == 0)
+                prev = j == 0 ? prev0 : __builtin_amdgcn_readlane(v[j - 1], 63);
+        }
+        d[j] = (t + 64u * j < n) ? T(v[j] - prev - 1u) : T(0);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j)
+        v[j] = d[j];
+}
+
 } // namespace tpf::dev
 
 // ============================================================== encoder

@@ -1,0 +1,242 @@
+// p4_server.hip -- resident block server for the per-block drop-in API
+// (include/turbopfor.h: one p4Enc* / p4Dec* call = one block).
+//
+// A launch plus a stream synchronise per call costs ~18-24 us on this stack
+// (DESIGN.md 5), 600x slower than the reference's own per-block call
+// (src/dispatch.cpp:88-95 on one core).  Here one workgroup stays resident
+// while calls keep coming: wave w polls mailbox w (tpf_server.h) in coherent
+// pinned host memory, decodes or encodes the block it finds with the generic
+// wave codec (p4_generic.h: every format of turbopfor.h; 256v64 = two
+// 128v64 blocks, p4enc256v64_scalar.cpp:15-30), writes the result back into
+// the mailbox and acknowledges.  Host and device exchange only plain loads
+// and stores ordered by system-scope fences (no atomics on host memory).
+// Exit: every wave leaves once all mailboxes have been idle for idle_ticks
+// of the 100 MHz real-time counter, or at once when the host sets `stop`;
+// the host relaunches on the next call.
+#include <hip/hip_runtime.h>
+
+#include "p4_generic.h"
+#include "tpf_kernels.h"
+#include "tpf_server.h"
+
+namespace tpf::dev
+{
+
+constexpr uint32_t kSrvImgU32 = (kServerPayload + 64u) / 4u;
+
+struct SrvLds
+{
+    uint32_t img[kSrvImgU32]; // staged block bytes (decode) / block image (encode)
+    uint64_t scr[512];        // vbyte exception scratch of decode_block_g
+    uint32_t hist[kPlanGHistU32];
+};
+
+// Host-memory words are read with (vector) atomic loads: a uniform plain load
+// could be turned into a scalar-cache load, which the fences do not refresh.
+__device__ __forceinline__ uint32_t ld_sys(const uint32_t * p)
+{
+    return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld_sys64(const uint64_t * p)
+{
+    return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Stage bytes [0, len) of a host buffer into LDS (and zero the 64 after).
+__device__ __forceinline__ void srv_stage(uint32_t * img, const uint8_t * src, uint32_t len, uint32_t t)
+{
+    const u32x4 * s = reinterpret_cast<const u32x4 *>(src);
+    u32x4 * d = reinterpret_cast<u32x4 *>(img);
+    const uint32_t n16 = (len + 15u) >> 4;
+    for (uint32_t i = t; i < n16 + 4u && i < kSrvImgU32 / 4u; i += 64u)
+        d[i] = i < n16 ? s[i] : u32x4{0u, 0u, 0u, 0u};
+    wave_lds_sync();
+    // bytes of the last chunk past len were read from the payload buffer: clear them
+    uint8_t * b = reinterpret_cast<uint8_t *>(img);
+    if (t < 16u && (len & 15u) && (len & ~15u) + t >= len)
+        b[(len & ~15u) + t] = 0;
+    wave_lds_sync();
+}
+
+// One F block at LDS byte s: values -> out (T), returns bytes consumed;
+// *lim = values the reference writes (n for a constant block, else the
+// layout's width).  D1: start -> *last (value n-1).
+template <Fmt F>
+__device__ __forceinline__ uint32_t srv_dec_one(SrvLds & L, uint32_t s, uint32_t n, bool d1, typename FmtTraits<F>::T start,
+                                                typename FmtTraits<F>::T * out, uint32_t t, uint32_t * lim,
+                                                typename FmtTraits<F>::T * last)
+{
+    using T = typename FmtTraits<F>::T;
+    const uint32_t NE = FmtTraits<F>::N ? FmtTraits<F>::N : n;
+    T v[4];
+    uint32_t cm;
+    const uint32_t used = decode_block_g<F>(L.img, s, n, L.scr, t, v, &cm);
+    if (d1)
+        *last = delta1_g<T>(v, n, start, t); // its carry: the value of element n-1
+    *lim = cm ? n : NE;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j)
+        if (t + 64u * j < *lim)
+            out[t + 64u * j] = v[j];
+    wave_lds_sync();
+    return used;
+}
+
+// One F block of n values from in (T, the layout's width) into the LDS
+// image at byte s (zeroed), returns its size.
+template <Fmt F>
+__device__ __forceinline__ uint32_t srv_enc_one(SrvLds & L, uint32_t s, const typename FmtTraits<F>::T * in, uint32_t n, bool d1,
+                                                typename FmtTraits<F>::T start, uint32_t t)
+{
+    using T = typename FmtTraits<F>::T;
+    const uint32_t NE = FmtTraits<F>::N ? FmtTraits<F>::N : n;
+    T v[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j)
+        v[j] = t + 64u * j < NE ? in[t + 64u * j] : T(0);
+    if (d1)
+        delta_enc_g<T>(v, start, n, t);
+    const PlanG P = plan_block_g<F>(v, n, L.hist, t);
+    emit_block_g<F>(L.img, s, P, v, n, t);
+    wave_lds_sync();
+    return P.size;
+}
+
+template <Fmt F>
+__device__ __forceinline__ void srv_serve(SrvLds & L, ServerBox * box, uint32_t op, uint32_t n, bool d1, uint64_t start,
+                                          uint32_t in_len, bool pair, uint32_t t)
+{
+    using T = typename FmtTraits<F>::T;
+    const uint32_t n0 = pair ? min(n, 128u) : n;
+    if (op == kOpDec)
+    {
+        srv_stage(L.img, box->in, in_len, t);
+        T * out = reinterpret_cast<T *>(box->out);
+        uint32_t lim = 0;
+        T last = T(0);
+        uint32_t used = srv_dec_one<F>(L, 0u, n0, d1, static_cast<T>(start), out, t, &lim, &last);
+        uint32_t written = lim;
+        if (pair && n > 128u)
+        {
+            // second 128v64 block, starting after the first one's value 127
+            used += srv_dec_one<F>(L, used, n - 128u, d1, last, out + 128, t, &lim, &last);
+            written = 128u + lim;
+        }
+        if (t == 0)
+        {
+            box->result = used == in_len ? used : 0xFFFFFFFFu;
+            box->written = written;
+        }
+        return;
+    }
+    // encode: values of the layout's width in box->in
+    const T * in = reinterpret_cast<const T *>(box->in);
+    const uint32_t zero16 = (kSrvImgU32 / 4u);
+    for (uint32_t i = t; i < zero16; i += 64u)
+        reinterpret_cast<u32x4 *>(L.img)[i] = u32x4{0u, 0u, 0u, 0u};
+    wave_lds_sync();
+    uint32_t size = srv_enc_one<F>(L, 0u, in, n0, d1, static_cast<T>(start), t);
+    if (pair && n > 128u)
+    {
+        // D1: the second block starts from input value 127 (p4d1enc256v64_scalar.cpp)
+        const T s127 = static_cast<T>(uni64(ld_sys64(reinterpret_cast<const uint64_t *>(in + 127))));
+        size += srv_enc_one<F>(L, size, in + 128, n - 128u, d1, s127, t);
+    }
+    // copy the image out (whole dwords: the mailbox payload is larger than any block)
+    uint32_t * dst = reinterpret_cast<uint32_t *>(box->out);
+    for (uint32_t i = t; i < (size + 3u) >> 2; i += 64u)
+        dst[i] = L.img[i];
+    if (t == 0)
+        box->result = size;
+}
+
+__global__ __launch_bounds__(256) void k_block_server(ServerCtl * ctl, uint64_t idle_ticks)
+{
+    __shared__ SrvLds L[kServerBoxes];
+    __shared__ uint64_t last_active;
+    __shared__ uint32_t quit;
+    const uint32_t t = threadIdx.x & 63u;
+    const uint32_t w = uni(threadIdx.x >> 6);
+    if (threadIdx.x == 0)
+    {
+        last_active = __builtin_amdgcn_s_memrealtime();
+        quit = 0u;
+    }
+    __syncthreads();
+    ServerBox * box = &ctl->box[w];
+    uint32_t last = uni(ld_sys(&box->ack));
+    for (uint32_t polls = 0;; ++polls)
+    {
+        const uint32_t r = uni(ld_sys(&box->req));
+        if (r != last)
+        {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // system scope: the request's fields and payload
+            const uint32_t op = uni(ld_sys(&box->op)), fmt = uni(ld_sys(&box->fmt)), n = uni(ld_sys(&box->n));
+            const uint32_t d1 = uni(ld_sys(&box->d1));
+            const uint64_t start = uni64(ld_sys64(&box->start));
+            const uint32_t in_len = uni(ld_sys(&box->in_len));
+            const bool ok = n >= 1u && n <= 256u && in_len <= kServerPayload;
+            if (!ok)
+            {
+                if (t == 0)
+                    box->result = 0xFFFFFFFFu;
+            }
+            else
+                switch (fmt)
+                {
+                    case FMT_32:
+                        srv_serve<Fmt::H32>(L[w], box, op, n, d1, start, in_len, false, t);
+                        break;
+                    case FMT_128V32:
+                        srv_serve<Fmt::V128>(L[w], box, op, min(n, 128u), d1, start, in_len, false, t);
+                        break;
+                    case FMT_256V32:
+                        srv_serve<Fmt::V256>(L[w], box, op, n, d1, start, in_len, false, t);
+                        break;
+                    case FMT_64:
+                        srv_serve<Fmt::H64>(L[w], box, op, n, d1, start, in_len, false, t);
+                        break;
+                    case FMT_128V64:
+                        srv_serve<Fmt::V128X64>(L[w], box, op, min(n, 128u), d1, start, in_len, false, t);
+                        break;
+                    case FMT_256V64:
+                        srv_serve<Fmt::V128X64>(L[w], box, op, n, d1, start, in_len, true, t);
+                        break;
+                    default:
+                        if (t == 0)
+                            box->result = 0xFFFFFFFFu;
+                }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); // results before the acknowledgement
+            if (t == 0)
+                __hip_atomic_store(&box->ack, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            last = r;
+            if (t == 0)
+                atomicMax(reinterpret_cast<unsigned long long *>(&last_active),
+                          static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+            continue;
+        }
+        // leave together: once one wave quits (idle or told to stop) the others follow
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        // (the stop word is read every 64th poll: each read is a PCIe round trip)
+        if (uni(quit) != 0u || ((polls & 63u) == 0u && uni(ld_sys(&ctl->stop)) != 0u) || now - last_active > idle_ticks)
+        {
+            if (t == 0)
+                quit = 1u;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+} // namespace tpf::dev
+
+namespace tpf
+{
+
+hipError_t launch_block_server(ServerCtl * d_ctl, hipStream_t s)
+{
+    hipLaunchKernelGGL(dev::k_block_server, dim3(1), dim3(256), 0, s, d_ctl, kServerIdleTicks);
+    return hipGetLastError();
+}
+
+} // namespace tpf

@@ -1,0 +1,58 @@
+// tpf_server.h -- mailbox layout of the per-block block server (shared by
+// p4_server.hip and host_api.cpp; internal).
+//
+// The per-block drop-in calls (include/turbopfor.h, one block per call) are
+// served by a resident kernel that polls mailboxes in coherent pinned host
+// memory, instead of one kernel launch plus one stream synchronise per call
+// (INTEGRATION.md 1).  Host and device exchange only plain
+// loads/stores ordered by fences -- no atomics on host memory:
+//   host  : payload and request fields, release, req = r
+//   device: sees req != last, acquire, serves, release, ack = r
+//   host  : sees ack == r, acquire, reads the result
+// The kernel exits once every mailbox has been idle for kServerIdleTicks of
+// the 100 MHz real-time clock (or at once when told to stop); the host sees
+// the launch complete and relaunches it on the next request.
+#pragma once
+
+#include <stdint.h>
+
+namespace tpf
+{
+
+constexpr uint32_t kServerBoxes = 4;          // one wave per mailbox, one workgroup
+constexpr uint32_t kServerPayload = 8192;     // bytes in / out per request
+constexpr uint64_t kServerIdleTicks = 1000000; // 10 ms of s_memrealtime (100 MHz)
+
+enum : uint32_t
+{
+    kOpDec = 0,
+    kOpEnc = 1,
+};
+
+struct alignas(128) ServerBox
+{
+    uint32_t req;  // host -> device: request number (monotonic, 0 = none yet)
+    uint32_t pad0[31];
+    uint32_t ack;  // device -> host: last request served
+    uint32_t pad1[31];
+    uint32_t op;   // kOpDec / kOpEnc
+    uint32_t fmt;  // TPF_FMT_*
+    uint32_t n;    // values per call
+    uint32_t d1;   // delta-1 variant
+    uint64_t start;  // D1 start
+    uint32_t in_len; // decode: block bytes; encode: value bytes
+    uint32_t result; // decode: bytes consumed; encode: bytes produced; 0xFFFFFFFF = malformed
+    uint32_t written; // decode: values written
+    uint32_t pad2[23];
+    uint8_t in[kServerPayload];
+    uint8_t out[kServerPayload];
+};
+
+struct alignas(128) ServerCtl
+{
+    uint32_t stop; // host -> device: exit now
+    uint32_t pad[31];
+    ServerBox box[kServerBoxes];
+};
+
+} // namespace tpf
