@@ -320,7 +320,8 @@ unsigned char * enc_srv(int fmt, const void * in, unsigned n, unsigned char * ou
     b->fmt = static_cast<uint32_t>(fmt);
     b->n = n;
     b->d1 = d1 ? 1u : 0u;
-    b->start = start;
+    b->start_lo = static_cast<uint32_t>(start);
+    b->start_hi = static_cast<uint32_t>(start >> 32);
     b->in_len = static_cast<uint32_t>(vbytes);
     S.call(L.i);
     const uint32_t size = b->result;
@@ -344,7 +345,8 @@ const unsigned char * dec_srv(int fmt, const unsigned char * in, unsigned n, voi
     b->fmt = static_cast<uint32_t>(fmt);
     b->n = n;
     b->d1 = d1 ? 1u : 0u;
-    b->start = start;
+    b->start_lo = static_cast<uint32_t>(start);
+    b->start_hi = static_cast<uint32_t>(start >> 32);
     b->in_len = static_cast<uint32_t>(size);
     S.call(L.i);
     if (b->result != size)

@@ -42,6 +42,11 @@ __device__ __forceinline__ uint64_t ld_sys64(const uint64_t * p)
     return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+__device__ __forceinline__ uint32_t rl32w(uint32_t v, uint32_t lane)
+{
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(lane)));
+}
+
 // Stage bytes [0, len) of a host buffer into LDS (and zero the 64 after).
 __device__ __forceinline__ void srv_stage(uint32_t * img, const uint8_t * src, uint32_t len, uint32_t t)
 {
@@ -165,16 +170,18 @@ __global__ __launch_bounds__(256) void k_block_server(ServerCtl * ctl, uint64_t 
     __syncthreads();
     ServerBox * box = &ctl->box[w];
     uint32_t last = uni(ld_sys(&box->ack));
+    const uint32_t * line = &box->req;
     for (uint32_t polls = 0;; ++polls)
     {
-        const uint32_t r = uni(ld_sys(&box->req));
+        // the whole request line in one read: lanes 0..7 hold its first 8 words
+        const uint32_t word = t < 8u ? ld_sys(line + t) : 0u;
+        const uint32_t r = rl32w(word, 0);
         if (r != last)
         {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // system scope: the request's fields and payload
-            const uint32_t op = uni(ld_sys(&box->op)), fmt = uni(ld_sys(&box->fmt)), n = uni(ld_sys(&box->n));
-            const uint32_t d1 = uni(ld_sys(&box->d1));
-            const uint64_t start = uni64(ld_sys64(&box->start));
-            const uint32_t in_len = uni(ld_sys(&box->in_len));
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // system scope: the payload
+            const uint32_t op = rl32w(word, 1), fmt = rl32w(word, 2), n = rl32w(word, 3);
+            const uint32_t d1 = rl32w(word, 4), in_len = rl32w(word, 5);
+            const uint64_t start = (static_cast<uint64_t>(rl32w(word, 7)) << 32) | rl32w(word, 6);
             const bool ok = n >= 1u && n <= 256u && in_len <= kServerPayload;
             if (!ok)
             {
@@ -224,7 +231,7 @@ __global__ __launch_bounds__(256) void k_block_server(ServerCtl * ctl, uint64_t 
                 quit = 1u;
             break;
         }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(1);
     }
 }
 

@@ -29,21 +29,26 @@ enum : uint32_t
     kOpEnc = 1,
 };
 
+// The request fields share ONE 64-byte line with the request number: the
+// host writes the fields, then (release) req; the device polls the whole
+// line's first 8 words with one 8-lane dword load (one read of the line,
+// which returns it as one unit), so a new req arrives with its fields.
 struct alignas(128) ServerBox
 {
-    uint32_t req;  // host -> device: request number (monotonic, 0 = none yet)
-    uint32_t pad0[31];
-    uint32_t ack;  // device -> host: last request served
-    uint32_t pad1[31];
-    uint32_t op;   // kOpDec / kOpEnc
-    uint32_t fmt;  // TPF_FMT_*
-    uint32_t n;    // values per call
-    uint32_t d1;   // delta-1 variant
-    uint64_t start;  // D1 start
-    uint32_t in_len; // decode: block bytes; encode: value bytes
-    uint32_t result; // decode: bytes consumed; encode: bytes produced; 0xFFFFFFFF = malformed
+    // --- request line (host -> device), 64 bytes
+    uint32_t req;     // request number (monotonic, 0 = none yet)
+    uint32_t op;      // kOpDec / kOpEnc
+    uint32_t fmt;     // TPF_FMT_*
+    uint32_t n;       // values per call
+    uint32_t d1;      // delta-1 variant
+    uint32_t in_len;  // decode: block bytes; encode: value bytes
+    uint32_t start_lo, start_hi; // D1 start
+    uint32_t pad0[24];
+    // --- answer line (device -> host)
+    uint32_t ack;     // last request served
+    uint32_t result;  // decode: bytes consumed; encode: bytes produced; 0xFFFFFFFF = malformed
     uint32_t written; // decode: values written
-    uint32_t pad2[23];
+    uint32_t pad1[29];
     uint8_t in[kServerPayload];
     uint8_t out[kServerPayload];
 };
