@@ -289,8 +289,15 @@ __device__ __forceinline__ uint32_t dsum_block256v32(const uint32_t * lds, uint3
             const uint32_t pc = __builtin_popcount(lds_u32(lds, s + 2u + 4u * (t & 7u)));
             const uint32_t xn = wave_sum((t < 8u) ? pc : 0u);
             const uint32_t xs = s + 34u;
-            for (uint32_t k = t; k < xn; k += kWave)
-                exsum += lds_bits(lds, xs * 8u + k * bx, bx);
+            // uniform trip count, predicated adds: a divergent per-lane loop
+            // costs exec-mask (SALU) work every block, and this pass is bound
+            // by its scalar issue (SQ_INSTS_SALU); lanes past xn
+            // read in-slot bytes and add nothing
+            for (uint32_t k0 = 0; k0 < xn; k0 += kWave)
+            {
+                const uint32_t x = lds_bits(lds, xs * 8u + (k0 + t) * bx, bx);
+                exsum += k0 + t < xn ? x : 0u;
+            }
             p = xs + ((xn * bx + 7u) >> 3);
         }
         used = p + 32u * b - s;
@@ -305,8 +312,11 @@ __device__ __forceinline__ uint32_t dsum_block256v32(const uint32_t * lds, uint3
         uint32_t vend;
         if (first == 0xFFu)
         {
-            for (uint32_t k = t; k < xn; k += kWave)
-                exsum += lds_u32(lds, v0 + 1u + 4u * k);
+            for (uint32_t k0 = 0; k0 < xn; k0 += kWave)
+            {
+                const uint32_t x = lds_u32(lds, v0 + 1u + 4u * (k0 + t));
+                exsum += k0 + t < xn ? x : 0u;
+            }
             vend = v0 + 1u + 4u * xn;
         }
         else
@@ -323,13 +333,14 @@ __device__ __forceinline__ uint32_t dsum_block256v32(const uint32_t * lds, uint3
                 const uint32_t cnt = min(m, xn - found);
                 const uint32_t qn = bperm(t + len0, q);
                 const uint32_t qe = q < 64u ? qn : q;
-                if (t < cnt)
                 {
+                    // every lane decodes (q <= 68: in-slot bytes), lanes >= cnt add nothing
                     const uint32_t by = lds_byte(lds, c + q);
                     const uint32_t d = lds_u32(lds, c + q + 1u);
                     const uint32_t v2 = ((by - 0x9Cu) << 8) + (d & 0xFFu) + 156u;
                     const uint32_t v3 = (d & 0xFFFFu) + ((by - 0xDCu) << 16) + 16540u;
-                    exsum += by < 0x9Cu ? by : by < 0xDCu ? v2 : by < 0xFCu ? v3 : by == 0xFCu ? (d & 0xFFFFFFu) : d;
+                    const uint32_t val = by < 0x9Cu ? by : by < 0xDCu ? v2 : by < 0xFCu ? v3 : by == 0xFCu ? (d & 0xFFFFFFu) : d;
+                    exsum += t < cnt ? val : 0u;
                 }
                 const uint32_t e_last = uni(__builtin_amdgcn_readlane(qe, cnt - 1u));
                 found += cnt;

@@ -12,8 +12,6 @@
 
 #include <hipcub/hipcub.hpp>
 
-#include <cstdlib>
-
 namespace tpf::dev
 {
 
@@ -157,59 +155,18 @@ namespace tpf
 
 namespace
 {
-// A/B knob (default = measured best): TPF_DEC_POL cache policy / block order
-// bits (see ld16/st16 in p4_dec_run.h).
-uint32_t env_knob(const char * name, uint32_t dflt)
-{
-    const char * e = std::getenv(name);
-    return e ? static_cast<uint32_t>(std::atoi(e)) : dflt;
-}
-
-uint32_t dec_pol()
-{
-    static const uint32_t v = env_knob("TPF_DEC_POL", 2u) & 7u;
-    return v;
-}
-
-// Layout of the loads in flight (A/B knob TPF_DEC_ONE, default 1): ONE =
-// one 16-byte load per lane per block (its first 1 KB; a bigger block's rest
-// is loaded when it is staged) with six blocks in flight, instead of two
-// loads per block (2 KB window) with three.  Same registers; measured on one
-// box, alternating: C2 899 -> 906, C3 1080 -> 1106 G int32/s, probes +0..4%.
-bool one_layout()
-{
-    static const uint32_t knob = env_knob("TPF_DEC_ONE", 1u);
-    return knob != 0u;
-}
-
-template <dev::StartMode SM, uint32_t POL>
-hipError_t launch_pol(const dev::DecArgs & A, hipStream_t stream)
-{
-    constexpr uint64_t per_wg = 4ull * dev::kRunDefault;
-    const uint32_t grid = static_cast<uint32_t>((A.nblocks + per_wg - 1) / per_wg);
-    if (one_layout())
-        hipLaunchKernelGGL((dev::k_dec256v32w<SM, dev::kRunDefault, POL, 6, 7, true>), dim3(grid), dim3(256), 0, stream, A);
-    else
-        hipLaunchKernelGGL((dev::k_dec256v32w<SM, dev::kRunDefault, POL>), dim3(grid), dim3(256), 0, stream, A);
-    return hipGetLastError();
-}
-
+// The measured best of round 1's A/B knobs, fixed (no environment switch on
+// the product path): non-temporal output stores, contiguous runs (POL 2),
+// one 16-byte load per lane per block with six blocks in flight (ONE / NC 6),
+// 7 waves per SIMD.  (C2 899 -> 906, C3 1080 -> 1106 G int32/s vs two loads
+// per block with three in flight)
 template <dev::StartMode SM>
 hipError_t launch_mode(const dev::DecArgs & A, hipStream_t stream)
 {
-    switch (dec_pol())
-    {
-        case 1:
-            return launch_pol<SM, 1>(A, stream);
-        case 0:
-            return launch_pol<SM, 0>(A, stream);
-        case 3:
-            return launch_pol<SM, 3>(A, stream);
-        case 6:
-            return launch_pol<SM, 6>(A, stream);
-        default:
-            return launch_pol<SM, 2>(A, stream);
-    }
+    constexpr uint64_t per_wg = 4ull * dev::kRunDefault;
+    const uint32_t grid = static_cast<uint32_t>((A.nblocks + per_wg - 1) / per_wg);
+    hipLaunchKernelGGL((dev::k_dec256v32w<SM, dev::kRunDefault, 2, 6, 7, true>), dim3(grid), dim3(256), 0, stream, A);
+    return hipGetLastError();
 }
 } // namespace
 
