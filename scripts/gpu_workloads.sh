@@ -1,9 +1,11 @@
-# Runs every bench workload once on one GPU (JSON lines -> gpurun_out/wl_*.json).
+# Bench lines of every workload on one GPU (JSON -> gpurun_out/$TAG_bench_*.json):
+# c2 with the end-to-end host legs, then c1 c3 c3chain c4 with their CPU baselines.
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R; mkdir -p gpurun_out
-timeout -k 10 400 python bench.py --e2e --sweep > gpurun_out/wl_c2.json 2> gpurun_out/wl_c2.err || { echo "c2 rc=$?"; tail -5 gpurun_out/wl_c2.err; exit 1; }
-cat gpurun_out/wl_c2.json
-for w in c1 c3 c3chain c4; do
-  timeout -k 10 300 python bench.py --workload $w --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/wl_$w.json 2> gpurun_out/wl_$w.err || { echo "$w rc=$?"; tail -5 gpurun_out/wl_$w.err; exit 1; }
-  cat gpurun_out/wl_$w.json
+T=${TAG:-wl}
+timeout -k 10 400 python bench.py --e2e --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/${T}_bench_c2_e2e.json 2> gpurun_out/${T}_c2_e2e.err || { echo "c2 e2e rc=$?"; tail -5 gpurun_out/${T}_c2_e2e.err; exit 1; }
+tail -1 gpurun_out/${T}_bench_c2_e2e.json
+for w in ${WLS:-c1 c3 c3chain c4}; do
+  timeout -k 10 300 python bench.py --workload $w --steps 10 --warmup 2 > gpurun_out/${T}_bench_$w.json 2> gpurun_out/${T}_$w.err || { echo "$w rc=$?"; tail -5 gpurun_out/${T}_$w.err; exit 1; }
+  tail -1 gpurun_out/${T}_bench_$w.json
 done
