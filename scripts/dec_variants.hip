@@ -1,0 +1,311 @@
+// dec_variants.hip -- measurement tool (not part of the library): variants of
+// the 256v32 decode kernel's work dealing, timed against the product kernel
+// on the same streams by scripts/dec_variants.py.  Same block machinery
+// (p4_dec_run.h / p4_block32.h); only which blocks a wave owns changes.
+//   DEAL 0: contiguous 16-block runs per wave (the product's layout)
+//   DEAL 1: a workgroup's 64 blocks dealt round-robin to its 4 waves
+//   DEAL 2: global stride: wave g owns blocks g + W*j (W = number of waves),
+//           so the resident waves write one contiguous window at a time
+//   DEAL 3: contiguous runs, workgroups remapped so each XCD takes one
+//           contiguous range of the stream (dispatch deals WGs round-robin)
+//   DEAL 4: global stride with 32 blocks per wave
+//   DEAL 5: contiguous runs, workgroups remapped in chunks of 8K: XCD x
+//           takes WGs [x*K, (x+1)*K) of each chunk (XCD-contiguous pieces of
+//           K workgroups, all XCDs moving through the stream together)
+// PROBE: the same loads and stores with the decoding removed.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++20 -shared -fPIC
+//        -I turbopfor-cpp_amd/csrc -o scripts/libdecvar.so scripts/dec_variants.hip
+#include "p4_dec_run.h"
+
+namespace tpf::dev
+{
+
+struct VArgs
+{
+    const uint8_t * in;
+    uint64_t in_bytes;
+    const uint64_t * off;
+    uint64_t nblocks;
+    uint32_t * out;
+    uint64_t waves; // DEAL 2: total waves
+    unsigned long long * err;
+};
+
+// ---- vbyte-path variants (VB template flag) -------------------------------
+//   VB bit 0: raw-escape exceptions read speculatively with the first byte
+//             (one LDS round trip less), accumulator cleared after use
+//             instead of before (no zeroing pass per block)
+//   VB bit 1: compressed windows with few values walked by a uniform
+//             v_readlane chain (p += len[p]) instead of binary lifting over
+//             ds_bpermute (11 dependent permutes per window)
+template <uint32_t VB>
+__device__ __forceinline__ uint32_t vbyte_exc_v(const uint32_t * lds, uint32_t v0, uint32_t xn, uint32_t * scr, uint32_t t,
+                                               uint32_t first, uint32_t rv, uint32_t rp)
+{
+    uint32_t * tmp = scr + 256;
+    if constexpr ((VB & 1u) == 0u)
+    {
+        reinterpret_cast<u32x4 *>(scr)[t] = u32x4{0u, 0u, 0u, 0u};
+        wave_lds_sync();
+    }
+    uint32_t vend;
+    if (first == 0xFFu)
+    {
+        const uint32_t pbase = v0 + 1u + 4u * xn;
+        if constexpr ((VB & 1u) != 0u)
+        {
+            if (t < xn)
+                atomicOr(&scr[rp], rv);
+            for (uint32_t k = t + kWave; k < xn; k += kWave)
+                atomicOr(&scr[lds_byte(lds, pbase + k)], lds_u32(lds, v0 + 1u + 4u * k));
+        }
+        else
+        {
+            for (uint32_t k = t; k < xn; k += kWave)
+                atomicOr(&scr[lds_byte(lds, pbase + k)], lds_u32(lds, v0 + 1u + 4u * k));
+        }
+        vend = pbase;
+    }
+    else
+    {
+        uint32_t c = v0, sp = 0, found = 0;
+        vend = v0;
+        while (found < xn)
+        {
+            const uint32_t by0 = lds_byte(lds, c + t);
+            const uint32_t len0 = by0 < 0x9Cu ? 1u : by0 < 0xDCu ? 2u : by0 < 0xFCu ? 3u : by0 == 0xFCu ? 4u : 5u;
+            const uint32_t need = xn - found;
+            uint32_t cnt, e_last;
+            bool st;
+            uint32_t rank;
+            if ((VB & 2u) != 0u && need <= 24u)
+            {
+                uint64_t S = 0u;
+                uint32_t p = sp;
+                cnt = 0u;
+                while (p < 64u && cnt < need)
+                {
+                    S |= 1ull << p;
+                    p += rl(len0, p);
+                    ++cnt;
+                }
+                e_last = p;
+                st = (S >> t) & 1u;
+                rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(S >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(S), 0u));
+            }
+            else
+            {
+                const uint32_t pk = window_starts(t + len0, sp, t);
+                const uint32_t m = static_cast<uint32_t>(__builtin_popcountll(__ballot(pk < 64u)));
+                cnt = min(m, need);
+                const uint32_t pn = bperm(t + len0, pk);
+                const uint32_t pe = pk < 64u ? pn : pk;
+                e_last = uni(__builtin_amdgcn_readlane(pe, cnt - 1u));
+                // express as "lane pk starts value t": decode in lane t at position pk
+                st = t < cnt;
+                rank = t;
+                if (st)
+                {
+                    const uint32_t by = lds_byte(lds, c + pk);
+                    const uint32_t d = lds_u32(lds, c + pk + 1u);
+                    const uint32_t v2 = ((by - 0x9Cu) << 8) + (d & 0xFFu) + 156u;
+                    const uint32_t v3 = (d & 0xFFFFu) + ((by - 0xDCu) << 16) + 16540u;
+                    tmp[(found + t) & 255u] = by < 0x9Cu ? by : by < 0xDCu ? v2 : by < 0xFCu ? v3 : by == 0xFCu ? (d & 0xFFFFFFu) : d;
+                }
+                st = false;
+            }
+            if (st)
+            {
+                const uint32_t by = by0;
+                const uint32_t d = lds_u32(lds, c + t + 1u);
+                const uint32_t v2 = ((by - 0x9Cu) << 8) + (d & 0xFFu) + 156u;
+                const uint32_t v3 = (d & 0xFFFFu) + ((by - 0xDCu) << 16) + 16540u;
+                tmp[(found + rank) & 255u] = by < 0x9Cu ? by : by < 0xDCu ? v2 : by < 0xFCu ? v3 : by == 0xFCu ? (d & 0xFFFFFFu) : d;
+            }
+            found += cnt;
+            vend = c + e_last;
+            sp = e_last >= 64u ? e_last - 64u : e_last;
+            c += e_last >= 64u ? 64u : 0u;
+        }
+        wave_lds_sync();
+        for (uint32_t k = t; k < xn; k += kWave)
+            atomicOr(&scr[lds_byte(lds, vend + k)], tmp[k]);
+    }
+    wave_lds_sync();
+    return vend + xn;
+}
+
+template <uint32_t VB>
+__device__ __forceinline__ uint32_t decode_block_v(const uint32_t * lds, uint32_t s, uint32_t hw, uint32_t * scr, uint32_t t, u32x4 & v)
+{
+    if constexpr (VB == 0u)
+        return decode_block256v32(lds, s, hw, scr, t, v);
+    const uint32_t h = hw & 0xFFu, x1 = (hw >> 8) & 0xFFu;
+    if ((h & 0xC0u) != 0x40u)
+        return decode_block256v32(lds, s, hw, scr, t, v);
+    const uint32_t b = min(h & 0x3Fu, 32u);
+    const uint32_t xn = x1;
+    const uint32_t v0 = s + 2u + 32u * b;
+    const uint32_t first = uni(lds_byte(lds, v0));
+    uint32_t rv = 0u, rp = 0u;
+    if constexpr ((VB & 1u) != 0u)
+    {
+        // raw-escape guess: value and position of exception t (in-slot bytes either way)
+        rv = lds_u32(lds, v0 + 1u + 4u * t);
+        rp = lds_byte(lds, v0 + 1u + 4u * xn + t);
+    }
+    v = unpack256v32_lane(lds, s + 2u, b, t);
+    const uint32_t end = vbyte_exc_v<VB>(lds, v0, xn, scr, t, first, rv, rp);
+    const u32x4 ex = reinterpret_cast<const u32x4 *>(scr)[t];
+    if constexpr ((VB & 1u) != 0u)
+        reinterpret_cast<u32x4 *>(scr)[t] = u32x4{0u, 0u, 0u, 0u};
+    v.x |= shl32(ex.x, b);
+    v.y |= shl32(ex.y, b);
+    v.z |= shl32(ex.z, b);
+    v.w |= shl32(ex.w, b);
+    return end - s;
+}
+
+template <int DEAL, bool PROBE, uint32_t kRun = 16, uint32_t K = 1, uint32_t VB = 0, uint32_t NC = 6, int MINW = 7>
+__global__ __launch_bounds__(256, MINW) void k_var(const VArgs A)
+{
+    __shared__ uint32_t slots[4][kSlotBytes / 4];
+    __shared__ uint32_t scratch[4][kWaveScratchU32];
+    const uint32_t t = threadIdx.x & 63u;
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    uint64_t wg = blockIdx.x;
+    if constexpr (DEAL == 3)
+    {
+        const uint64_t G = gridDim.x, q = G / 8u, r = G % 8u, x = wg % 8u, k = wg / 8u;
+        wg = x * q + (x < r ? x : r) + k;
+    }
+    if constexpr (DEAL == 5)
+    {
+        const uint64_t G = gridDim.x, base = wg / (8u * K) * (8u * K), Gc = min_u64(8u * K, G - base), i = wg - base;
+        const uint64_t q = Gc / 8u, r = Gc % 8u, x = i % 8u, k = i / 8u;
+        wg = base + x * q + (x < r ? x : r) + k;
+    }
+    uint32_t * slot = slots[wv];
+    uint32_t * scr = scratch[wv];
+    if constexpr ((VB & 1u) != 0u)
+        reinterpret_cast<u32x4 *>(scr)[t] = u32x4{0u, 0u, 0u, 0u};
+    const uint64_t in_base = reinterpret_cast<uint64_t>(A.in);
+    const uint64_t in_end = in_base + A.in_bytes;
+
+    uint64_t first, stride;
+    if constexpr (DEAL == 1)
+    {
+        first = wg * 4u * kRun + wv;
+        stride = 4u;
+    }
+    else if constexpr (DEAL == 2 || DEAL == 4)
+    {
+        first = wg * 4u + wv;
+        stride = A.waves;
+    }
+    else
+    {
+        first = (wg * 4u + wv) * kRun;
+        stride = 1u;
+    }
+    if (first >= A.nblocks || ((DEAL == 2 || DEAL == 4) && first >= A.waves))
+        return;
+    const uint32_t n = static_cast<uint32_t>(min_u64(kRun, (A.nblocks - first + stride - 1u) / stride));
+
+    const bool valid = t < n;
+    const uint64_t blk = first + stride * t;
+    const uint64_t o = valid ? A.off[blk] : 0ull;
+    const uint64_t e = valid ? A.off[blk + 1u] : 0ull;
+    RunPlaneT<kSlotBytes, true> P;
+    P.init(in_base, in_end, o, e, valid);
+    uint32_t * const out_run = A.out + first * 256u;
+    uint64_t badmask = 0u;
+
+    auto issue = [&](Chunk & c, uint32_t jj) { P.template issue<2>(c, jj, t); };
+    auto consume = [&](const Chunk & c, uint32_t jj) {
+        u32x4 * dst = reinterpret_cast<u32x4 *>(out_run + jj * stride * 256u) + t;
+        if constexpr (PROBE)
+        {
+            st16<2>(dst, c.a | P.big_rest_or(jj, t));
+            return;
+        }
+        const uint32_t ctl = P.stage(c, jj, slot, t);
+        u32x4 v;
+        const uint32_t used = decode_block_v<VB>(slot, (ctl >> kCtlShift) & 15u, P.head(c, ctl, slot), scr, t, v);
+        st16<2>(dst, v);
+        wave_lds_sync();
+        if (used != rl(P.len, jj))
+            badmask |= 1ull << jj;
+    };
+    Chunk C[NC];
+#pragma unroll
+    for (uint32_t u = 0; u + 1 < NC; ++u)
+        issue(C[u], u);
+    bool more = true;
+    for (uint32_t j = 0; more; j += NC)
+    {
+#pragma unroll
+        for (uint32_t u = 0; u < NC; ++u)
+        {
+            if (more)
+            {
+                issue(C[(u + NC - 1) % NC], j + u + NC - 1);
+                consume(C[u], j + u);
+                more = j + u + 1 < n;
+            }
+        }
+    }
+    if (A.err != nullptr && t == 0 && badmask != 0u)
+        atomicMin(A.err, static_cast<unsigned long long>(first + stride * __builtin_ctzll(badmask)));
+}
+
+template <int DEAL, bool PROBE, uint32_t K = 1, uint32_t VB = 0>
+int launch_var(const VArgs & A0, hipStream_t s)
+{
+    constexpr uint32_t kRun = DEAL == 4 ? 32u : 16u;
+    VArgs A = A0;
+    const uint64_t waves = (A.nblocks + kRun - 1u) / kRun;
+    A.waves = waves;
+    const uint32_t grid = static_cast<uint32_t>((waves + 3u) / 4u);
+    hipLaunchKernelGGL((k_var<DEAL, PROBE, kRun, K, VB>), dim3(grid), dim3(256), 0, s, A);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+} // namespace tpf::dev
+
+extern "C" int decvar_launch(int deal, int probe, const void * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, void * out,
+                             unsigned long long * err, void * stream)
+{
+    using namespace tpf::dev;
+    const VArgs A{static_cast<const uint8_t *>(in), in_bytes, off, nblocks, static_cast<uint32_t *>(out), 0u, err};
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    if (nblocks == 0)
+        return 0;
+    switch (deal * 2 + (probe ? 1 : 0))
+    {
+        case 0: return launch_var<0, false>(A, s);
+        case 1: return launch_var<0, true>(A, s);
+        case 2: return launch_var<1, false>(A, s);
+        case 3: return launch_var<1, true>(A, s);
+        case 4: return launch_var<2, false>(A, s);
+        case 5: return launch_var<2, true>(A, s);
+        case 6: return launch_var<3, false>(A, s);
+        case 7: return launch_var<3, true>(A, s);
+        case 8: return launch_var<4, false>(A, s);
+        case 9: return launch_var<4, true>(A, s);
+        case 10: return launch_var<5, false, 2>(A, s);
+        case 11: return launch_var<5, true, 2>(A, s);
+        case 12: return launch_var<5, false, 8>(A, s);
+        case 13: return launch_var<5, true, 8>(A, s);
+        case 14: return launch_var<5, false, 32>(A, s);
+        case 15: return launch_var<5, true, 32>(A, s);
+        case 16: return launch_var<5, false, 128>(A, s);
+        case 17: return launch_var<5, true, 128>(A, s);
+        case 18: return launch_var<5, false, 512>(A, s);
+        case 19: return launch_var<5, true, 512>(A, s);
+        case 20: return launch_var<0, false, 1, 1>(A, s);
+        case 22: return launch_var<0, false, 1, 2>(A, s);
+        case 24: return launch_var<0, false, 1, 3>(A, s);
+        default: return -2;
+    }
+}
