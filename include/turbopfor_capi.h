@@ -53,11 +53,14 @@ const unsigned char *tpf_p4Dec256v64(const unsigned char *in, unsigned n, uint64
 const unsigned char *tpf_p4D1Dec256v64(const unsigned char *in, unsigned n, uint64_t *out, uint64_t start);
 
 /* How the per-block calls above reach the GPU (identical bytes either way):
- * 0 (default) = a resident block server kernel polling mailboxes in coherent
- * pinned host memory (no launch per call; it exits after 10 ms without
- * calls and is relaunched on the next one), 1 = one batched launch plus a
- * stream synchronise per call.  mode < 0 only queries.  Returns the
- * previous mode. */
+ * 0 (default) = a resident block server kernel (no launch per call; it exits
+ * after 10 ms without calls and is relaunched on the next one) whose request
+ * mailboxes sit in fine-grained device memory the host writes through the
+ * BAR, answers in pinned host memory; 2 = the same server with the request
+ * mailboxes in pinned host memory (the kernel polls across PCIe); 1 = one
+ * batched launch plus a stream synchronise per call.  mode < 0 only queries.
+ * Switch between calls, not while a per-block call is in flight.  Returns
+ * the previous mode. */
 int tpf_perblock_mode(int mode);
 
 /* ---- stream framing (host, no decoding) -------------------

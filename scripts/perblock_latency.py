@@ -2,7 +2,10 @@
 p4Enc256v32 (and the 32-bit p4Dec32 of configs[0]) through their extern "C"
 mirrors, one block per call, as a reference caller relinked against
 libturbopfor_amd.so would call them, for both per-block designs
-(tpf_perblock_mode 0 = resident block server, 1 = launch + synchronise).
+(tpf_perblock_mode 0 = resident block server with request mailboxes in
+device memory, 2 = the same with request mailboxes in host memory, 1 =
+launch + synchronise).  The first line times a bare ctypes call (the
+Python-side share of every number).
 Prints the median and p99 over `calls` calls.
 usage: python scripts/perblock_latency.py [calls]"""
 import ctypes
@@ -36,7 +39,13 @@ L.tpf_p4Enc32.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]
 v127 = rng.integers(0, 256, 127, dtype=np.uint32)
 b127 = np.zeros(1024, np.uint8)
 o127 = np.zeros(256, np.uint32)
-for mode, mname in ((1, "launch+sync"), (0, "block server")):
+ts = np.empty(calls)
+for i in range(calls):
+    t0 = time.perf_counter()
+    L.tpf_perblock_mode(-1)
+    ts[i] = time.perf_counter() - t0
+print(f"bare ctypes call (tpf_perblock_mode(-1)): median {np.median(ts) * 1e6:6.2f} us")
+for mode, mname in ((1, "launch+sync"), (2, "server/hostmail"), (0, "block server")):
     L.tpf_perblock_mode(mode)
     L.tpf_p4Enc32(v127.ctypes.data, 127, b127.ctypes.data)
     for name, fn in (("p4Enc256v32", lambda: L.tpf_p4Enc256v32(vals.ctypes.data, 256, buf.ctypes.data)),
@@ -49,7 +58,7 @@ for mode, mname in ((1, "launch+sync"), (0, "block server")):
             t0 = time.perf_counter()
             fn()
             ts[i] = time.perf_counter() - t0
-        print(f"{mname:13s} {name:14s}: median {np.median(ts) * 1e6:6.1f} us, p99 {np.percentile(ts, 99) * 1e6:6.1f} us, "
+        print(f"{mname:15s} {name:14s}: median {np.median(ts) * 1e6:6.1f} us, p99 {np.percentile(ts, 99) * 1e6:6.1f} us, "
               f"mean {ts.mean() * 1e6:6.1f} us per call")
     assert np.array_equal(out, vals) and np.array_equal(o127[:127], v127)
 L.tpf_perblock_mode(0)

@@ -27,10 +27,12 @@ def capi():
     return L
 
 
-@pytest.fixture(params=[0, 1], ids=["server", "launch"])
+@pytest.fixture(params=[0, 1, 2], ids=["server", "launch", "server-hostmail"])
 def perblock_mode(request):
-    """Both per-block designs (tpf_perblock_mode): the resident block server
-    (default) and one launch + synchronise per call."""
+    """Every per-block design (tpf_perblock_mode): the resident block server
+    with request mailboxes in device memory (default), one launch +
+    synchronise per call, and the server with request mailboxes in host
+    memory."""
     L = capi()
     L.tpf_perblock_mode.restype = ctypes.c_int
     L.tpf_perblock_mode.argtypes = [ctypes.c_int]

@@ -6,14 +6,17 @@
 //
 // Per-block calls (one block per call, as reference callers chain them) go
 // to the resident block server (p4_server.hip, tpf_server.h): the call
-// copies the block into a mailbox in coherent pinned host memory, bumps the
-// request word and spins until the kernel acknowledges -- no launch, no
-// stream synchronise per call.  tpf_perblock_mode(1) selects the first
-// design instead (a thread-local stream and pinned staging, one batched
-// launch with nblocks = 1 on the staging's device addresses, synchronise:
-// 18-24 us per call, the launch + synchronise floor).  Both give identical
-// bytes; throughput callers use tpf_host_dec/tpf_host_enc (pipelined host
-// streams) or turbopfor_gpu.h (device-resident batches).
+// writes the block into a request mailbox in fine-grained device memory
+// (through the BAR), bumps the request word and spins on the acknowledgement
+// in pinned host memory -- no launch, no stream synchronise per call.
+// tpf_perblock_mode(2) keeps the request mailboxes in pinned host memory
+// (the first server layout: the kernel polls across PCIe);
+// tpf_perblock_mode(1) selects the first design (a thread-local stream and
+// pinned staging, one batched launch with nblocks = 1 on the staging's
+// device addresses, synchronise: 18-25 us per call, the launch + synchronise
+// floor).  All give identical bytes; throughput callers use
+// tpf_host_dec/tpf_host_enc (pipelined host streams) or turbopfor_gpu.h
+// (device-resident batches).
 #include <hip/hip_runtime.h>
 #include <immintrin.h>
 
@@ -163,7 +166,9 @@ struct Ctx
 };
 
 // ---- resident block server (per device) ------------------------------------
-std::atomic<int> g_mode{0}; // 0 = block server, 1 = launch + synchronise per call
+// 0 = block server with request mailboxes in device memory, 1 = launch +
+// synchronise per call, 2 = block server with request mailboxes in host memory
+std::atomic<int> g_mode{0};
 
 struct Server
 {
@@ -171,32 +176,55 @@ struct Server
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr; // recorded after the current launch
     bool launched = false;
-    tpf::ServerCtl * h = nullptr; // coherent pinned mailboxes (host view)
-    tpf::ServerCtl * d = nullptr; // the same memory, device view
-    std::mutex mu;                // launches, event queries, mailbox leases
+    // request halves: fine-grained device memory written through the BAR
+    // (mode 0; its host and device addresses coincide) and pinned host memory
+    // (mode 2)
+    tpf::ServerReq * rq_dev = nullptr;
+    tpf::ServerReq * rq_host = nullptr;
+    tpf::ServerReq * rq_host_d = nullptr;
+    tpf::ServerAns * an = nullptr;   // answers: coherent pinned host memory (host view)
+    tpf::ServerAns * an_d = nullptr; // the same memory, device view
+    std::atomic<tpf::ServerReq *> launched_rq{nullptr};
+    std::mutex mu; // launches, event queries, mailbox leases
     std::condition_variable cv;
     uint32_t free_mask = (1u << tpf::kServerBoxes) - 1u;
-    uint32_t reqno[tpf::kServerBoxes] = {};
+    std::atomic<uint32_t> reqno[tpf::kServerBoxes] = {};
+
+    static void * pinned(size_t bytes, void ** dev_view)
+    {
+        void * p = nullptr;
+        hip_check(hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocPortable), "server mailboxes");
+        std::memset(p, 0, bytes);
+        hip_check(hipHostGetDevicePointer(dev_view, p, 0), "server mailbox device address");
+        return p;
+    }
 
     explicit Server(int device) : dev(device)
     {
         hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "server stream");
         hip_check(hipEventCreateWithFlags(&done, hipEventDisableTiming), "server event");
-        void * p = nullptr;
-        hip_check(hipHostMalloc(&p, sizeof(tpf::ServerCtl), hipHostMallocCoherent | hipHostMallocPortable), "mailboxes");
-        std::memset(p, 0, sizeof(tpf::ServerCtl));
-        h = static_cast<tpf::ServerCtl *>(p);
-        void * dp = nullptr;
-        hip_check(hipHostGetDevicePointer(&dp, p, 0), "mailbox device address");
-        d = static_cast<tpf::ServerCtl *>(dp);
+        void * dv = nullptr;
+        an = static_cast<tpf::ServerAns *>(pinned(sizeof(tpf::ServerAns), &dv));
+        an_d = static_cast<tpf::ServerAns *>(dv);
+        rq_host = static_cast<tpf::ServerReq *>(pinned(sizeof(tpf::ServerReq), &dv));
+        rq_host_d = static_cast<tpf::ServerReq *>(dv);
+        void * q = nullptr;
+        hip_check(hipExtMallocWithFlags(&q, sizeof(tpf::ServerReq), hipDeviceMallocFinegrained), "request mailboxes");
+        hip_check(hipMemsetAsync(q, 0, sizeof(tpf::ServerReq), stream), "request mailboxes");
+        hip_check(hipStreamSynchronize(stream), "request mailboxes");
+        rq_dev = static_cast<tpf::ServerReq *>(q);
     }
 
-    // caller holds mu
-    void launch()
+    // the request half the current mode uses (host view)
+    tpf::ServerReq * current() const { return g_mode.load(std::memory_order_relaxed) == 2 ? rq_host : rq_dev; }
+
+    // caller holds mu, no launch running
+    void launch(tpf::ServerReq * rq)
     {
-        hip_check(tpf::launch_block_server(d, stream), "block server launch");
+        hip_check(tpf::launch_block_server(rq == rq_host ? rq_host_d : rq, an_d, stream), "block server launch");
         hip_check(hipEventRecord(done, stream), "block server event");
         launched = true;
+        launched_rq.store(rq, std::memory_order_release);
     }
     // caller holds mu: has the current launch ended (idle exit or stop)?
     bool ended()
@@ -208,6 +236,34 @@ struct Server
             return false;
         hip_check(e, "block server");
         return true;
+    }
+    // caller holds mu
+    void stop_locked()
+    {
+        tpf::ServerReq * rq = launched_rq.load(std::memory_order_acquire);
+        if (!launched || rq == nullptr)
+            return;
+        __atomic_store_n(&rq->stop, 1u, __ATOMIC_RELEASE);
+        _mm_sfence();
+        (void)hipEventSynchronize(done);
+        __atomic_store_n(&rq->stop, 0u, __ATOMIC_RELEASE);
+        _mm_sfence();
+    }
+    // Mode switch (no call in flight): retire the launch and bring both
+    // request halves' numbers up to date -- a half unused for a while holds
+    // stale request words, which a new launch would take for new requests.
+    void switch_halves()
+    {
+        std::lock_guard<std::mutex> g(mu);
+        stop_locked();
+        for (uint32_t i = 0; i < tpf::kServerBoxes; ++i)
+        {
+            const uint32_t r = reqno[i].load();
+            __atomic_store_n(&rq_dev->box[i].req, r, __ATOMIC_RELAXED);
+            __atomic_store_n(&rq_host->box[i].req, r, __ATOMIC_RELAXED);
+        }
+        _mm_sfence();
+        std::atomic_thread_fence(std::memory_order_seq_cst);
     }
 
     int lease()
@@ -227,30 +283,40 @@ struct Server
         cv.notify_one();
     }
 
-    // Post the request prepared in mailbox i and wait for its acknowledgement.
-    void call(int i)
+    // Make sure a launch serves `rq`.  Fast path: the running launch raised
+    // `alive` and polls this request half -- no event query, no lock.
+    void ensure(tpf::ServerReq * rq)
     {
-        tpf::ServerBox * b = &h->box[i];
-        const uint32_t r = ++reqno[i];
-        {
-            std::lock_guard<std::mutex> g(mu);
-            if (ended())
-                launch();
-        }
+        if (__atomic_load_n(&an->alive, __ATOMIC_ACQUIRE) != 0u && launched_rq.load(std::memory_order_acquire) == rq)
+            return;
+        std::lock_guard<std::mutex> g(mu);
+        if (ended())
+            launch(rq);
+    }
+
+    // Post the request prepared in box i of `rq` and wait for its acknowledgement.
+    void call(tpf::ServerReq * rq, int i)
+    {
+        tpf::ServerReqBox * b = &rq->box[i];
+        tpf::ServerAnsBox * a = &an->box[i];
+        const uint32_t r = reqno[i].fetch_add(1u) + 1u;
+        ensure(rq);
+        _mm_sfence(); // the payload and fields (write-combined device memory) before the request word
         std::atomic_thread_fence(std::memory_order_release);
         __atomic_store_n(&b->req, r, __ATOMIC_RELEASE);
+        _mm_sfence();
         const auto t0 = std::chrono::steady_clock::now();
         for (uint64_t spin = 1;; ++spin)
         {
-            if (__atomic_load_n(&b->ack, __ATOMIC_ACQUIRE) == r)
+            if (__atomic_load_n(&a->ack, __ATOMIC_ACQUIRE) == r)
                 break;
             _mm_pause();
             if ((spin & 1023u) == 0u)
             {
                 // the launch may have idled out just before this request: relaunch
                 std::lock_guard<std::mutex> g(mu);
-                if (ended() && __atomic_load_n(&b->ack, __ATOMIC_ACQUIRE) != r)
-                    launch();
+                if (ended() && __atomic_load_n(&a->ack, __ATOMIC_ACQUIRE) != r)
+                    launch(rq);
                 if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20))
                     throw std::runtime_error("turbopfor_amd: block server did not answer within 20 s");
             }
@@ -261,10 +327,7 @@ struct Server
     void stop()
     {
         std::lock_guard<std::mutex> g(mu);
-        __atomic_store_n(&h->stop, 1u, __ATOMIC_RELEASE);
-        if (launched)
-            (void)hipEventSynchronize(done);
-        __atomic_store_n(&h->stop, 0u, __ATOMIC_RELEASE);
+        stop_locked();
     }
 };
 
@@ -302,17 +365,20 @@ Server & server()
 struct BoxLease
 {
     Server & s;
+    tpf::ServerReq * rq;
     int i;
-    explicit BoxLease(Server & srv) : s(srv), i(srv.lease()) { }
+    explicit BoxLease(Server & srv) : s(srv), rq(srv.current()), i(srv.lease()) { }
     ~BoxLease() { s.release(i); }
-    tpf::ServerBox * box() const { return &s.h->box[i]; }
+    tpf::ServerReqBox * req() const { return &rq->box[i]; }
+    tpf::ServerAnsBox * ans() const { return &s.an->box[i]; }
+    void call() { s.call(rq, i); }
 };
 
 unsigned char * enc_srv(int fmt, const void * in, unsigned n, unsigned char * out, bool d1, uint64_t start)
 {
     Server & S = server();
     BoxLease L(S);
-    tpf::ServerBox * b = L.box();
+    tpf::ServerReqBox * b = L.req();
     const size_t es = wide_fmt(fmt) ? 8 : 4;
     const size_t vbytes = es * unit_values(fmt, n); // the reference also reads the full block width
     std::memcpy(b->in, in, vbytes);
@@ -323,11 +389,12 @@ unsigned char * enc_srv(int fmt, const void * in, unsigned n, unsigned char * ou
     b->start_lo = static_cast<uint32_t>(start);
     b->start_hi = static_cast<uint32_t>(start >> 32);
     b->in_len = static_cast<uint32_t>(vbytes);
-    S.call(L.i);
-    const uint32_t size = b->result;
+    L.call();
+    const tpf::ServerAnsBox * a = L.ans();
+    const uint32_t size = a->result;
     if (size == 0xFFFFFFFFu || size > tpf::kServerPayload)
         throw std::runtime_error("turbopfor_amd: block server rejected the encode request");
-    std::memcpy(out, b->out, size);
+    std::memcpy(out, a->out, size);
     return out + size;
 }
 
@@ -339,7 +406,7 @@ const unsigned char * dec_srv(int fmt, const unsigned char * in, unsigned n, voi
         throw std::runtime_error("turbopfor_amd: malformed P4 block header");
     Server & S = server();
     BoxLease L(S);
-    tpf::ServerBox * b = L.box();
+    tpf::ServerReqBox * b = L.req();
     std::memcpy(b->in, in, size);
     b->op = tpf::kOpDec;
     b->fmt = static_cast<uint32_t>(fmt);
@@ -348,11 +415,12 @@ const unsigned char * dec_srv(int fmt, const unsigned char * in, unsigned n, voi
     b->start_lo = static_cast<uint32_t>(start);
     b->start_hi = static_cast<uint32_t>(start >> 32);
     b->in_len = static_cast<uint32_t>(size);
-    S.call(L.i);
-    if (b->result != size)
+    L.call();
+    const tpf::ServerAnsBox * a = L.ans();
+    if (a->result != size)
         throw std::runtime_error("turbopfor_amd: malformed P4 block (length check failed on the device)");
     const size_t es = wide_fmt(fmt) ? 8 : 4;
-    std::memcpy(out, b->out, es * b->written);
+    std::memcpy(out, a->out, es * a->written);
     return in + size;
 }
 
@@ -364,7 +432,7 @@ unsigned char * enc_one(int fmt, const void * in, unsigned n, unsigned char * ou
 {
     if (n == 0)
         return out;
-    if (g_mode.load(std::memory_order_relaxed) == 0)
+    if (g_mode.load(std::memory_order_relaxed) != 1)
         return enc_srv(fmt, in, n, out, d1, start);
     Ctx & c = Ctx::get();
     const size_t es = wide_fmt(fmt) ? 8 : 4;
@@ -391,7 +459,7 @@ const unsigned char * dec_one(int fmt, const unsigned char * in, unsigned n, voi
 {
     if (n == 0)
         return in;
-    if (g_mode.load(std::memory_order_relaxed) == 0)
+    if (g_mode.load(std::memory_order_relaxed) != 1)
         return dec_srv(fmt, in, n, out, d1, start);
     Ctx & c = Ctx::get();
     int written = 0;
@@ -551,7 +619,18 @@ extern "C" {
 
 int tpf_perblock_mode(int mode)
 {
-    return mode >= 0 ? g_mode.exchange(mode == 1 ? 1 : 0) : g_mode.load();
+    if (mode < 0)
+        return g_mode.load();
+    const int m = mode == 1 || mode == 2 ? mode : 0;
+    const int old = g_mode.exchange(m);
+    if (old != m)
+    {
+        std::lock_guard<std::mutex> g(g_srv_mu);
+        for (Server * s : g_srv)
+            if (s)
+                s->switch_halves();
+    }
+    return old;
 }
 
 #define TPF_MIRROR_ENC(NAME, T)                                                                                  \

@@ -4,15 +4,16 @@
 // A launch plus a stream synchronise per call costs ~18-24 us on this stack
 // (DESIGN.md 5), 600x slower than the reference's own per-block call
 // (src/dispatch.cpp:88-95 on one core).  Here one workgroup stays resident
-// while calls keep coming: wave w polls mailbox w (tpf_server.h) in coherent
-// pinned host memory, decodes or encodes the block it finds with the generic
-// wave codec (p4_generic.h: every format of turbopfor.h; 256v64 = two
-// 128v64 blocks, p4enc256v64_scalar.cpp:15-30), writes the result back into
-// the mailbox and acknowledges.  Host and device exchange only plain loads
-// and stores ordered by system-scope fences (no atomics on host memory).
-// Exit: every wave leaves once all mailboxes have been idle for idle_ticks
-// of the 100 MHz real-time counter, or at once when the host sets `stop`;
-// the host relaunches on the next call.
+// while calls keep coming: wave w polls request box w (tpf_server.h: in
+// fine-grained device memory the host writes through the BAR, or in pinned
+// host memory), decodes or encodes the block it finds with the generic wave
+// codec (p4_generic.h: every format of turbopfor.h; 256v64 = two 128v64
+// blocks, p4enc256v64_scalar.cpp:15-30), writes the result into answer box w
+// in pinned host memory and acknowledges.  Host and device exchange only
+// plain loads and stores ordered by system-scope fences (no atomics on
+// shared memory).  Exit: every wave leaves once all mailboxes have been idle
+// for idle_ticks of the 100 MHz real-time counter, or at once when the host
+// sets `stop`; `alive` drops and the host relaunches on the next call.
 #include <hip/hip_runtime.h>
 
 #include "p4_generic.h"
@@ -31,7 +32,7 @@ struct SrvLds
     uint32_t hist[kPlanGHistU32];
 };
 
-// Host-memory words are read with (vector) atomic loads: a uniform plain load
+// Mailbox words are read with (vector) atomic loads: a uniform plain load
 // could be turned into a scalar-cache load, which the fences do not refresh.
 __device__ __forceinline__ uint32_t ld_sys(const uint32_t * p)
 {
@@ -108,15 +109,15 @@ __device__ __forceinline__ uint32_t srv_enc_one(SrvLds & L, uint32_t s, const ty
 }
 
 template <Fmt F>
-__device__ __forceinline__ void srv_serve(SrvLds & L, ServerBox * box, uint32_t op, uint32_t n, bool d1, uint64_t start,
-                                          uint32_t in_len, bool pair, uint32_t t)
+__device__ __forceinline__ void srv_serve(SrvLds & L, const ServerReqBox * box, ServerAnsBox * ans, uint32_t op, uint32_t n,
+                                          bool d1, uint64_t start, uint32_t in_len, bool pair, uint32_t t)
 {
     using T = typename FmtTraits<F>::T;
     const uint32_t n0 = pair ? min(n, 128u) : n;
     if (op == kOpDec)
     {
         srv_stage(L.img, box->in, in_len, t);
-        T * out = reinterpret_cast<T *>(box->out);
+        T * out = reinterpret_cast<T *>(ans->out);
         uint32_t lim = 0;
         T last = T(0);
         uint32_t used = srv_dec_one<F>(L, 0u, n0, d1, static_cast<T>(start), out, t, &lim, &last);
@@ -129,8 +130,8 @@ __device__ __forceinline__ void srv_serve(SrvLds & L, ServerBox * box, uint32_t 
         }
         if (t == 0)
         {
-            box->result = used == in_len ? used : 0xFFFFFFFFu;
-            box->written = written;
+            ans->result = used == in_len ? used : 0xFFFFFFFFu;
+            ans->written = written;
         }
         return;
     }
@@ -148,14 +149,14 @@ __device__ __forceinline__ void srv_serve(SrvLds & L, ServerBox * box, uint32_t 
         size += srv_enc_one<F>(L, size, in + 128, n - 128u, d1, s127, t);
     }
     // copy the image out (whole dwords: the mailbox payload is larger than any block)
-    uint32_t * dst = reinterpret_cast<uint32_t *>(box->out);
+    uint32_t * dst = reinterpret_cast<uint32_t *>(ans->out);
     for (uint32_t i = t; i < (size + 3u) >> 2; i += 64u)
         dst[i] = L.img[i];
     if (t == 0)
-        box->result = size;
+        ans->result = size;
 }
 
-__global__ __launch_bounds__(256) void k_block_server(ServerCtl * ctl, uint64_t idle_ticks)
+__global__ __launch_bounds__(256) void k_block_server(ServerReq * rq, ServerAns * an, uint64_t idle_ticks)
 {
     __shared__ SrvLds L[kServerBoxes];
     __shared__ uint64_t last_active;
@@ -167,9 +168,12 @@ __global__ __launch_bounds__(256) void k_block_server(ServerCtl * ctl, uint64_t 
         last_active = __builtin_amdgcn_s_memrealtime();
         quit = 0u;
     }
+    if (threadIdx.x == 0)
+        __hip_atomic_store(&an->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __syncthreads();
-    ServerBox * box = &ctl->box[w];
-    uint32_t last = uni(ld_sys(&box->ack));
+    const ServerReqBox * box = &rq->box[w];
+    ServerAnsBox * ans = &an->box[w];
+    uint32_t last = uni(ld_sys(&ans->ack));
     const uint32_t * line = &box->req;
     for (uint32_t polls = 0;; ++polls)
     {
@@ -186,36 +190,36 @@ __global__ __launch_bounds__(256) void k_block_server(ServerCtl * ctl, uint64_t 
             if (!ok)
             {
                 if (t == 0)
-                    box->result = 0xFFFFFFFFu;
+                    ans->result = 0xFFFFFFFFu;
             }
             else
                 switch (fmt)
                 {
                     case FMT_32:
-                        srv_serve<Fmt::H32>(L[w], box, op, n, d1, start, in_len, false, t);
+                        srv_serve<Fmt::H32>(L[w], box, ans, op, n, d1, start, in_len, false, t);
                         break;
                     case FMT_128V32:
-                        srv_serve<Fmt::V128>(L[w], box, op, min(n, 128u), d1, start, in_len, false, t);
+                        srv_serve<Fmt::V128>(L[w], box, ans, op, min(n, 128u), d1, start, in_len, false, t);
                         break;
                     case FMT_256V32:
-                        srv_serve<Fmt::V256>(L[w], box, op, n, d1, start, in_len, false, t);
+                        srv_serve<Fmt::V256>(L[w], box, ans, op, n, d1, start, in_len, false, t);
                         break;
                     case FMT_64:
-                        srv_serve<Fmt::H64>(L[w], box, op, n, d1, start, in_len, false, t);
+                        srv_serve<Fmt::H64>(L[w], box, ans, op, n, d1, start, in_len, false, t);
                         break;
                     case FMT_128V64:
-                        srv_serve<Fmt::V128X64>(L[w], box, op, min(n, 128u), d1, start, in_len, false, t);
+                        srv_serve<Fmt::V128X64>(L[w], box, ans, op, min(n, 128u), d1, start, in_len, false, t);
                         break;
                     case FMT_256V64:
-                        srv_serve<Fmt::V128X64>(L[w], box, op, n, d1, start, in_len, true, t);
+                        srv_serve<Fmt::V128X64>(L[w], box, ans, op, n, d1, start, in_len, true, t);
                         break;
                     default:
                         if (t == 0)
-                            box->result = 0xFFFFFFFFu;
+                            ans->result = 0xFFFFFFFFu;
                 }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); // results before the acknowledgement
             if (t == 0)
-                __hip_atomic_store(&box->ack, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&ans->ack, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             last = r;
             if (t == 0)
                 atomicMax(reinterpret_cast<unsigned long long *>(&last_active),
@@ -225,7 +229,7 @@ __global__ __launch_bounds__(256) void k_block_server(ServerCtl * ctl, uint64_t 
         // leave together: once one wave quits (idle or told to stop) the others follow
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
         // (the stop word is read every 64th poll: each read is a PCIe round trip)
-        if (uni(quit) != 0u || ((polls & 63u) == 0u && uni(ld_sys(&ctl->stop)) != 0u) || now - last_active > idle_ticks)
+        if (uni(quit) != 0u || ((polls & 63u) == 0u && uni(ld_sys(&rq->stop)) != 0u) || now - last_active > idle_ticks)
         {
             if (t == 0)
                 quit = 1u;
@@ -233,6 +237,10 @@ __global__ __launch_bounds__(256) void k_block_server(ServerCtl * ctl, uint64_t 
         }
         __builtin_amdgcn_s_sleep(1);
     }
+    // every wave has left its poll loop: no request is served after this point
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(&an->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 } // namespace tpf::dev
@@ -240,9 +248,9 @@ __global__ __launch_bounds__(256) void k_block_server(ServerCtl * ctl, uint64_t 
 namespace tpf
 {
 
-hipError_t launch_block_server(ServerCtl * d_ctl, hipStream_t s)
+hipError_t launch_block_server(ServerReq * d_req, ServerAns * d_ans, hipStream_t s)
 {
-    hipLaunchKernelGGL(dev::k_block_server, dim3(1), dim3(256), 0, s, d_ctl, kServerIdleTicks);
+    hipLaunchKernelGGL(dev::k_block_server, dim3(1), dim3(256), 0, s, d_req, d_ans, kServerIdleTicks);
     return hipGetLastError();
 }
 

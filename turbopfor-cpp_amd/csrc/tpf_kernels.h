@@ -33,8 +33,9 @@ hipError_t launch_append(uint8_t * dst, const uint8_t * src, const uint64_t * po
                          hipStream_t s);
 hipError_t launch_err_merge(unsigned long long * err, const unsigned long long * sub_err, uint64_t base, hipStream_t s);
 // Per-block block server (p4_server.hip, tpf_server.h).
-struct ServerCtl;
-hipError_t launch_block_server(ServerCtl * d_ctl, hipStream_t s);
+struct ServerReq;
+struct ServerAns;
+hipError_t launch_block_server(ServerReq * d_req, ServerAns * d_ans, hipStream_t s);
 // Measurement only: streaming read / write / copy ceilings (hbm_probe.hip).
 hipError_t launch_probe_hbm(int kind, void * dst, const void * src, uint64_t bytes, hipStream_t s);
 

@@ -2,16 +2,25 @@
 // p4_server.hip and host_api.cpp; internal).
 //
 // The per-block drop-in calls (include/turbopfor.h, one block per call) are
-// served by a resident kernel that polls mailboxes in coherent pinned host
-// memory, instead of one kernel launch plus one stream synchronise per call
-// (INTEGRATION.md 1).  Host and device exchange only plain
-// loads/stores ordered by fences -- no atomics on host memory:
-//   host  : payload and request fields, release, req = r
+// served by a resident kernel that polls mailboxes, instead of one kernel
+// launch plus one stream synchronise per call.
+// Each mailbox has two halves:
+//   ServerReq (host -> device): request line + input payload.  Placed in
+//     fine-grained DEVICE memory that the host writes through the BAR, so the
+//     kernel polls and stages from its own HBM instead of reading across PCIe
+//     (tpf_perblock_mode 0; mode 2 keeps it in coherent pinned host memory).
+//   ServerAns (device -> host): answer line + output payload, always in
+//     coherent pinned host memory, so the host polls its own cache.
+// Host and device exchange only plain loads/stores ordered by fences -- no
+// atomics on shared memory:
+//   host  : payload and request fields, release (+ sfence), req = r
 //   device: sees req != last, acquire, serves, release, ack = r
 //   host  : sees ack == r, acquire, reads the result
-// The kernel exits once every mailbox has been idle for kServerIdleTicks of
-// the 100 MHz real-time clock (or at once when told to stop); the host sees
-// the launch complete and relaunches it on the next request.
+// The kernel raises ServerAns::alive while it runs (the host posts without
+// querying the launch's event) and exits once every mailbox has been idle for
+// kServerIdleTicks of the 100 MHz real-time clock (or at once when told to
+// stop); the host sees alive drop / the launch complete and relaunches it on
+// the next request.
 #pragma once
 
 #include <stdint.h>
@@ -19,8 +28,8 @@
 namespace tpf
 {
 
-constexpr uint32_t kServerBoxes = 4;          // one wave per mailbox, one workgroup
-constexpr uint32_t kServerPayload = 8192;     // bytes in / out per request
+constexpr uint32_t kServerBoxes = 4;           // one wave per mailbox, one workgroup
+constexpr uint32_t kServerPayload = 8192;      // bytes in / out per request
 constexpr uint64_t kServerIdleTicks = 1000000; // 10 ms of s_memrealtime (100 MHz)
 
 enum : uint32_t
@@ -30,12 +39,11 @@ enum : uint32_t
 };
 
 // The request fields share ONE 64-byte line with the request number: the
-// host writes the fields, then (release) req; the device polls the whole
-// line's first 8 words with one 8-lane dword load (one read of the line,
-// which returns it as one unit), so a new req arrives with its fields.
-struct alignas(128) ServerBox
+// host writes the fields, then (release) req; the device polls the line's
+// first 8 words with one 8-lane dword load (one read of the line, which
+// returns it as one unit), so a new req arrives with its fields.
+struct alignas(128) ServerReqBox
 {
-    // --- request line (host -> device), 64 bytes
     uint32_t req;     // request number (monotonic, 0 = none yet)
     uint32_t op;      // kOpDec / kOpEnc
     uint32_t fmt;     // TPF_FMT_*
@@ -44,20 +52,30 @@ struct alignas(128) ServerBox
     uint32_t in_len;  // decode: block bytes; encode: value bytes
     uint32_t start_lo, start_hi; // D1 start
     uint32_t pad0[24];
-    // --- answer line (device -> host)
+    uint8_t in[kServerPayload];
+};
+
+struct alignas(128) ServerAnsBox
+{
     uint32_t ack;     // last request served
     uint32_t result;  // decode: bytes consumed; encode: bytes produced; 0xFFFFFFFF = malformed
     uint32_t written; // decode: values written
     uint32_t pad1[29];
-    uint8_t in[kServerPayload];
     uint8_t out[kServerPayload];
 };
 
-struct alignas(128) ServerCtl
+struct alignas(128) ServerReq
 {
     uint32_t stop; // host -> device: exit now
     uint32_t pad[31];
-    ServerBox box[kServerBoxes];
+    ServerReqBox box[kServerBoxes];
+};
+
+struct alignas(128) ServerAns
+{
+    uint32_t alive; // device -> host: 1 while a launch is serving
+    uint32_t pad[31];
+    ServerAnsBox box[kServerBoxes];
 };
 
 } // namespace tpf
