@@ -279,3 +279,38 @@ def test_per_block_server_concurrent_threads():
     for t in ts:
         t.join(timeout=120)
     assert not errors, errors
+
+
+def test_per_block_server_idle_exit_and_mode_switch():
+    """The block server leaves after 10 ms without a request and the next call
+    relaunches it; switching between the server layouts (device / host
+    request mailboxes) and launch + synchronise between calls keeps every
+    answer exact (stale request words of the unused layout must not be taken
+    for new requests)."""
+    import time
+
+    L = capi()
+    L.tpf_perblock_mode.restype = ctypes.c_int
+    L.tpf_perblock_mode.argtypes = [ctypes.c_int]
+    L.tpf_p4Enc256v32.restype = ctypes.c_void_p
+    L.tpf_p4Enc256v32.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]
+    L.tpf_p4Dec256v32.restype = ctypes.c_void_p
+    L.tpf_p4Dec256v32.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]
+    prev = L.tpf_perblock_mode(-1)
+    blocks = datagen.c2_blocks(12, 9, 10, seed=5)
+    try:
+        for step, mode in enumerate([0, 0, 2, 2, 1, 0, 2, 0]):
+            L.tpf_perblock_mode(mode)
+            for v in blocks[step % 3::3]:
+                v = np.ascontiguousarray(v)
+                buf = np.zeros(4096, np.uint8)
+                end = L.tpf_p4Enc256v32(v.ctypes.data, 256, buf.ctypes.data)
+                assert end is not None
+                assert bytes(buf[: end - buf.ctypes.data]) == oracle_lib.encode("256v32", v)
+                out = np.zeros(256, np.uint32)
+                assert L.tpf_p4Dec256v32(buf.ctypes.data, 256, out.ctypes.data) == end
+                assert np.array_equal(out, v), (step, mode)
+            if step in (1, 3, 6):
+                time.sleep(0.05)  # past the server's 10 ms idle exit
+    finally:
+        L.tpf_perblock_mode(prev)

@@ -132,9 +132,7 @@ int tpf_p4d1dec256v32_batch(const uint8_t * d_in, uint64_t in_bytes, const uint6
     return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_p4d1dec256v32_batch");
 }
 
-static size_t incl_bytes(uint64_t nblocks) { return (nblocks * 4u + 255u) & ~size_t(255); }
-
-size_t tpf_p4d1dec256v32_chain_workspace_size(uint64_t nblocks) { return incl_bytes(nblocks) + tpf::d1chain_workspace(nblocks); }
+size_t tpf_p4d1dec256v32_chain_workspace_size(uint64_t nblocks) { return tpf::d1chain_workspace(nblocks); }
 
 int tpf_p4d1dec256v32_chain_sums(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nblocks, void * d_ws,
                                  size_t ws_bytes, uint32_t * d_total, uint64_t * d_err, void * stream)
@@ -148,12 +146,8 @@ int tpf_p4d1dec256v32_chain_sums(const uint8_t * d_in, uint64_t in_bytes, const 
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (int rc = prep_err(d_err, s))
         return rc;
-    auto * incl = static_cast<uint32_t *>(d_ws);
-    void * tmp = static_cast<uint8_t *>(d_ws) + incl_bytes(nblocks);
-    hipError_t e = tpf::launch_d1chain_sums(d_in, in_bytes, d_off, nblocks, incl, tmp, ws_bytes - incl_bytes(nblocks),
+    hipError_t e = tpf::launch_d1chain_sums(d_in, in_bytes, d_off, nblocks, d_ws, ws_bytes, d_total,
                                             reinterpret_cast<unsigned long long *>(d_err), s);
-    if (e == hipSuccess && d_total)
-        e = nblocks ? hipMemcpyAsync(d_total, incl + (nblocks - 1), 4, hipMemcpyDeviceToDevice, s) : hipMemsetAsync(d_total, 0, 4, s);
     return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_p4d1dec256v32_chain_sums");
 }
 
@@ -167,7 +161,7 @@ int tpf_p4d1dec256v32_chain_decode(const uint8_t * d_in, uint64_t in_bytes, cons
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (int rc = prep_err(d_err, s))
         return rc;
-    hipError_t e = tpf::launch_d1chain_decode(d_in, in_bytes, d_off, nblocks, d_out, static_cast<const uint32_t *>(d_ws), base,
+    hipError_t e = tpf::launch_d1chain_decode(d_in, in_bytes, d_off, nblocks, d_out, d_ws, base,
                                               reinterpret_cast<unsigned long long *>(d_err), s);
     return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_p4d1dec256v32_chain_decode");
 }

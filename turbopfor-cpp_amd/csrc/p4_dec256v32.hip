@@ -10,7 +10,7 @@
 #include "p4_dec_run.h"
 #include "tpf_kernels.h"
 
-#include <hipcub/hipcub.hpp>
+#include "p4_scan.h"
 
 namespace tpf::dev
 {
@@ -19,7 +19,7 @@ enum class StartMode : int
 {
     None = 0,     // p4Dec256v32
     PerBlock = 1, // p4D1Dec256v32, start of block i = starts[i]
-    Prefix = 2,   // chained list: start of block i = base + incl[i-1] (incl = prefix of block sums)
+    Prefix = 2,   // chained list: start of block i = base + sum of the block sums before i (run scan, p4_scan.h)
     SumOnly = 3,  // no output: sums[i] = sum over the block of (v + 1) mod 2^32
     Probe = 4,    // measurement only: same loads and stores, no decode (data-movement ceiling)
 };
@@ -31,10 +31,13 @@ struct DecArgs
     const uint64_t * off;
     uint64_t nblocks;
     uint32_t * out;
-    const uint32_t * starts; // PerBlock: starts; Prefix: inclusive block-sum prefix
+    const uint32_t * starts; // PerBlock: starts; Prefix: the block sums of phase A
     uint32_t base;           // Prefix: value preceding block 0
-    uint32_t * sums;         // SumOnly
+    uint32_t * sums;         // SumOnly: block sums
     unsigned long long * err;
+    uint32_t * run_tot = nullptr;        // SumOnly: one sum per wave run
+    const uint32_t * run_pre = nullptr;  // Prefix: run scan (p4_scan.h)
+    const uint32_t * run_tile = nullptr; // Prefix: run scan (p4_scan.h)
 };
 
 // ---------------------------------------------------------------------------
@@ -82,7 +85,11 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
     if constexpr (SM == StartMode::PerBlock)
         startv = valid ? A.starts[blk] : 0u;
     if constexpr (SM == StartMode::Prefix)
-        startv = A.base + ((valid && blk > 0) ? A.starts[blk - 1u] : 0u);
+    {
+        // base + the run's base + the sums of the run's earlier blocks (mod 2^32)
+        const uint32_t sv = valid ? A.starts[blk] : 0u;
+        startv = A.base + run_base(A.run_pre, A.run_tile, first / kRun) + (wave_incl_scan(sv) - sv);
+    }
     uint32_t sumv = 0u;
     uint32_t * const out_run = SM == StartMode::SumOnly ? nullptr : A.out + first * 256u;
     uint64_t badmask = 0u;
@@ -143,6 +150,7 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
     {
         if (valid)
             A.sums[blk] = sumv;
+        publish_run_total(A.run_tot, first / kRun, valid ? sumv : 0u, t);
     }
     if (A.err != nullptr && t == 0 && badmask != 0u)
         atomicMin(A.err, static_cast<unsigned long long>(first + stride * __builtin_ctzll(badmask)));
@@ -189,38 +197,47 @@ hipError_t launch_dec256v32(const uint8_t * in, uint64_t in_bytes, const uint64_
 }
 
 // Chained delta-1: phase A computes every block's sum of
-// (v+1) and their inclusive prefix in `incl` (device, nblocks u32); phase B
-// decodes with start(i) = base + incl[i-1].  A shard of a multi-GPU list runs
-// A, exchanges its total incl[n-1] with the other ranks, then B with its base.
-size_t d1chain_workspace(uint64_t nblocks)
+// (v+1) and one sum per 16-block wave run, the run sums are scanned
+// (p4_scan.h, mod 2^32); phase B decodes with start(i) = base + the run's
+// base + the sums of the run's blocks before i.  A shard of a multi-GPU list
+// runs A, exchanges its total with the other ranks, then B with its base.
+// Workspace: block sums (u32) + the run scan.
+namespace
 {
-    size_t scan_bytes = 0;
-    (void)hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes, static_cast<uint32_t *>(nullptr), static_cast<uint32_t *>(nullptr),
-                                           static_cast<int>(std::min<uint64_t>(nblocks, 0x7FFFFFFF)));
-    return scan_bytes + 256;
-}
+uint64_t chain_runs(uint64_t nblocks) { return (nblocks + dev::kRunDefault - 1u) / dev::kRunDefault; }
+size_t al256(size_t x) { return (x + 255u) & ~size_t(255); }
+} // namespace
 
-hipError_t launch_d1chain_sums(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * incl,
-                               void * ws, size_t ws_bytes, unsigned long long * err, hipStream_t stream)
+size_t d1chain_workspace(uint64_t nblocks) { return al256(nblocks * 4u) + RunScanWs<uint32_t>::bytes(chain_runs(nblocks)); }
+
+hipError_t launch_d1chain_sums(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, void * ws, size_t ws_bytes,
+                               uint32_t * total, unsigned long long * err, hipStream_t stream)
 {
     if (nblocks == 0)
-        return hipSuccess;
-    if (nblocks > 0x7FFFFFFFull)
+        return total ? hipMemsetAsync(total, 0, 4, stream) : hipSuccess;
+    if (nblocks > 0x7FFFFFFFull || ws_bytes < d1chain_workspace(nblocks))
         return hipErrorInvalidValue;
-    const dev::DecArgs A{in, in_bytes, off, nblocks, nullptr, nullptr, 0u, incl, err};
+    auto * sums = static_cast<uint32_t *>(ws);
+    const RunScanWs<uint32_t> rs = RunScanWs<uint32_t>::carve(static_cast<uint8_t *>(ws) + al256(nblocks * 4u), chain_runs(nblocks));
+    dev::DecArgs A{in, in_bytes, off, nblocks, nullptr, nullptr, 0u, sums, err};
+    A.run_tot = rs.tot;
     hipError_t e = launch_mode<dev::StartMode::SumOnly>(A, stream);
     if (e != hipSuccess)
         return e;
-    size_t sb = ws_bytes;
-    return hipcub::DeviceScan::InclusiveSum(ws, sb, incl, incl, static_cast<int>(nblocks), stream);
+    return launch_run_scan_u32(rs.tot, chain_runs(nblocks), rs.pre, rs.tile, total, stream);
 }
 
 hipError_t launch_d1chain_decode(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * out,
-                                 const uint32_t * incl, uint32_t base, unsigned long long * err, hipStream_t stream)
+                                 const void * ws, uint32_t base, unsigned long long * err, hipStream_t stream)
 {
     if (nblocks == 0)
         return hipSuccess;
-    const dev::DecArgs A{in, in_bytes, off, nblocks, out, incl, base, nullptr, err};
+    const auto * sums = static_cast<const uint32_t *>(ws);
+    const RunScanWs<uint32_t> rs =
+        RunScanWs<uint32_t>::carve(const_cast<uint8_t *>(static_cast<const uint8_t *>(ws)) + al256(nblocks * 4u), chain_runs(nblocks));
+    dev::DecArgs A{in, in_bytes, off, nblocks, out, sums, base, nullptr, err};
+    A.run_pre = rs.pre;
+    A.run_tile = rs.tile;
     return launch_mode<dev::StartMode::Prefix>(A, stream);
 }
 

@@ -2,15 +2,19 @@
 // p4D1Enc256v32, reference src/scalar/p4enc256v32_scalar.cpp:216-235 and
 // p4d1enc256v32_scalar.cpp:7-15) on gfx950.
 //
-// Three launches:
+// Four launches:
 //   1. plan  : one wave per block evaluates p4Bits32 (parallel cost model,
-//              p4_enc32.h) and the exact encoded size -> d_off[i], plan word.
-//   2. scan  : exclusive sum of sizes in place (hipcub/rocPRIM) -> byte offsets.
-//   3. write : one wave per block scatters header, bitmap / exceptions / base
-//              payload / vbytes into a zeroed LDS image whose dword phase
-//              matches the destination, then streams it out with dword stores
-//              (byte stores only on the two edge dwords shared with the
-//              neighbouring blocks).
+//              p4_enc32.h) and the exact encoded size -> d_off[i], plan word,
+//              and one byte total per 16-block wave run.
+//   2,3. run scan (p4_scan.h): exclusive prefix of the run totals only (two
+//              small kernels over 1/16 of the entries; a library device scan
+//              over every block's size cost 0.08 ms per 10M blocks).
+//   4. write : rebuilds its run's offsets (run base + wave scan of the
+//              sizes) and writes them to d_off; one wave per block scatters
+//              header, bitmap / exceptions / base payload / vbytes into a
+//              zeroed LDS image whose dword phase matches the destination,
+//              then streams it out with dword stores (byte stores only on the
+//              two edge dwords shared with the neighbouring blocks).
 // Both kernels walk runs of 16 consecutive blocks per wave with the values of
 // the next two blocks in flight (the first version loaded one block per loop
 // iteration and waited for it: 5.0 and 5.4 ms per 10M blocks, latency-bound).
@@ -21,7 +25,7 @@
 // copying the staged values instead of building blocks; same loads and
 // stores, so they time each pass's data-movement ceiling
 // (scripts/gpu_enc_probe.sh, profiles/r1_v4_enc_probe.txt).
-#include <hipcub/hipcub.hpp>
+#include "p4_scan.h"
 
 #include "p4_enc32.h"
 #include "tpf_kernels.h"
@@ -196,17 +200,19 @@ __device__ __forceinline__ void write_run(const EncRun & R, const uint32_t * in,
     });
 }
 
-// ---- two-pass encoder (plan -> hipcub scan -> write): the production path ---
+// ---- two-pass encoder (plan -> run scan -> write): the production path ---
+// The plan pass leaves each block's size in off[block] and one total per
+// wave run; p4_scan.h scans only the run totals; the write pass rebuilds the
+// offsets of its run from the run base and its sizes and writes them back.
 template <bool D1, int PROBE = 0>
 __global__ __launch_bounds__(256) void k_enc256v32_plan(const uint32_t * __restrict in, uint64_t nblocks,
                                                          const uint32_t * __restrict starts, uint32_t start0,
-                                                         uint64_t * __restrict sizes, uint32_t * __restrict plan)
+                                                         uint64_t * __restrict sizes, uint32_t * __restrict plan,
+                                                         uint32_t * __restrict run_tot)
 {
     __shared__ __attribute__((aligned(16))) uint32_t hist[4][kPlanHistU32];
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
-    if (blockIdx.x == 0 && threadIdx.x == 0)
-        sizes[nblocks] = 0; // exclusive scan over nblocks+1 entries yields the total
     EncRun R;
     if (!R.init(in, nblocks, wv))
         return;
@@ -217,12 +223,14 @@ __global__ __launch_bounds__(256) void k_enc256v32_plan(const uint32_t * __restr
         sizes[R.first + t] = szv;
         plan[R.first + t] = pwv;
     }
+    publish_run_total(run_tot, R.first / kEncRun, t < R.n ? szv : 0u, t);
 }
 
 template <bool D1, int PROBE = 0>
 __global__ __launch_bounds__(256) void k_enc256v32_write(const uint32_t * __restrict in, uint64_t nblocks,
                                                           const uint32_t * __restrict starts, uint32_t start0,
-                                                          const uint64_t * __restrict off, const uint32_t * __restrict plan,
+                                                          uint64_t * __restrict off, const uint32_t * __restrict plan,
+                                                          const uint64_t * __restrict run_pre, const uint64_t * __restrict run_tile,
                                                           uint8_t * __restrict out, uint64_t out_cap)
 {
     __shared__ __attribute__((aligned(16))) uint32_t img_all[4][kImgU32];
@@ -234,8 +242,8 @@ __global__ __launch_bounds__(256) void k_enc256v32_write(const uint32_t * __rest
     if (!R.init(in, nblocks, wv))
         return;
     // lane j: destination offset (64-bit), size and plan of block first+j
-    const uint64_t ov = t < R.n ? off[R.first + t] : 0ull;
-    const uint64_t ev = t < R.n ? off[R.first + t + 1u] : 0ull;
+    uint64_t ov, ev;
+    run_offsets(off, R.first, R.n, run_base(run_pre, run_tile, R.first / kEncRun), t, ov, ev);
     const uint32_t szv = static_cast<uint32_t>(ev - ov);
     const uint32_t pwv = t < R.n ? plan[R.first + t] : 0u;
     zero_image(img, kImgU32 / 4u, t);
@@ -544,14 +552,10 @@ namespace
 
 size_t al256(size_t x) { return (x + 255u) & ~size_t(255); }
 
-// two-pass encoder workspace: plan words + hipcub scan temp
-size_t twopass_workspace(uint64_t nblocks)
-{
-    size_t scan_bytes = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, static_cast<uint64_t *>(nullptr),
-                                     static_cast<int>(std::min<uint64_t>(nblocks + 1, 0x7FFFFFFF)));
-    return al256(nblocks * 4u) + scan_bytes + 256;
-}
+uint64_t enc_runs(uint64_t nblocks) { return (nblocks + dev::kEncRun - 1u) / dev::kEncRun; }
+
+// two-pass encoder workspace: plan words + the run scan (p4_scan.h)
+size_t twopass_workspace(uint64_t nblocks) { return al256(nblocks * 4u) + RunScanWs<uint64_t>::bytes(enc_runs(nblocks)); }
 
 struct PipeGeom
 {
@@ -692,33 +696,35 @@ hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_
                   : launch_pipe_w<false>(minw, in, nblocks, starts, start0, out, out_cap, off, ws, stream, ci, lag, per_ticket);
     }
     // the production two-pass encoder (probe 0 / 3), or its passes with the coding removed (probe 1 / 2)
+    if (ws_bytes < twopass_workspace(nblocks))
+        return hipErrorInvalidValue;
     uint32_t * plan = static_cast<uint32_t *>(ws);
-    const size_t plan_bytes = al256(nblocks * 4u);
-    void * scan_tmp = static_cast<uint8_t *>(ws) + plan_bytes;
-    size_t scan_bytes = ws_bytes > plan_bytes ? ws_bytes - plan_bytes : 0;
+    const uint64_t nruns = enc_runs(nblocks);
+    const RunScanWs<uint64_t> rs = RunScanWs<uint64_t>::carve(static_cast<uint8_t *>(ws) + al256(nblocks * 4u), nruns);
     const uint64_t per_wg = 4ull * dev::kEncRun;
     const uint32_t grid = static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg);
     if (d1)
-        hipLaunchKernelGGL(dev::k_enc256v32_plan<true>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan);
+        hipLaunchKernelGGL(dev::k_enc256v32_plan<true>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan, rs.tot);
     else if (probe == 1)
-        hipLaunchKernelGGL((dev::k_enc256v32_plan<false, 1>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan);
+        hipLaunchKernelGGL((dev::k_enc256v32_plan<false, 1>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
+                           rs.tot);
     else
-        hipLaunchKernelGGL(dev::k_enc256v32_plan<false>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan);
+        hipLaunchKernelGGL(dev::k_enc256v32_plan<false>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan, rs.tot);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return e;
-    e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, off, static_cast<int>(nblocks + 1), stream);
+    e = launch_run_scan_u64(rs.tot, nruns, rs.pre, rs.tile, off + nblocks, stream);
     if (e != hipSuccess)
         return e;
     if (d1)
-        hipLaunchKernelGGL(dev::k_enc256v32_write<true>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
-                           out, out_cap);
+        hipLaunchKernelGGL(dev::k_enc256v32_write<true>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan, rs.pre,
+                           rs.tile, out, out_cap);
     else if (probe == 2)
         hipLaunchKernelGGL((dev::k_enc256v32_write<false, 2>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
-                           out, out_cap);
+                           rs.pre, rs.tile, out, out_cap);
     else
         hipLaunchKernelGGL(dev::k_enc256v32_write<false>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
-                           out, out_cap);
+                           rs.pre, rs.tile, out, out_cap);
     return hipGetLastError();
 }
 

@@ -11,7 +11,7 @@
 // Each block is built in its own LDS image whose dword phase puts the base
 // payload on a dword (a 256v64 unit's second block starts at an arbitrary
 // byte), then copied out (copy_out_image16, p4_enc32.h).
-#include <hipcub/hipcub.hpp>
+#include "p4_scan.h"
 
 #include "p4_generic.h"
 #include "tpf_kernels.h"
@@ -337,13 +337,12 @@ __device__ __forceinline__ void unit_values(const Chunk64 & c, uint64_t start, u
 template <uint32_t NB, bool D1>
 __global__ __launch_bounds__(256) void k_enc128v64_plan(const uint64_t * __restrict in, uint64_t nunits,
                                                         const uint64_t * __restrict starts, uint64_t start0,
-                                                        uint64_t * __restrict sizes, uint64_t * __restrict plan)
+                                                        uint64_t * __restrict sizes, uint64_t * __restrict plan,
+                                                        uint32_t * __restrict run_tot)
 {
     __shared__ __attribute__((aligned(16))) uint32_t hist[4][kPlanGHistU32];
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
-    if (blockIdx.x == 0 && threadIdx.x == 0)
-        sizes[nunits] = 0; // exclusive scan over nunits+1 entries yields the total
     EncRun64<NB> R;
     if (!R.init(in, nunits, wv))
         return;
@@ -370,12 +369,14 @@ __global__ __launch_bounds__(256) void k_enc128v64_plan(const uint64_t * __restr
         sizes[R.first + t] = szv;
         plan[R.first + t] = pwv;
     }
+    publish_run_total(run_tot, R.first / kEnc64Run, t < R.n ? szv : 0u, t);
 }
 
 template <uint32_t NB, bool D1>
 __global__ __launch_bounds__(256) void k_enc128v64_write(const uint64_t * __restrict in, uint64_t nunits,
                                                          const uint64_t * __restrict starts, uint64_t start0,
-                                                         const uint64_t * __restrict off, const uint64_t * __restrict plan,
+                                                         uint64_t * __restrict off, const uint64_t * __restrict plan,
+                                                         const uint64_t * __restrict run_pre, const uint64_t * __restrict run_tile,
                                                          uint8_t * __restrict out, uint64_t out_cap)
 {
     __shared__ __attribute__((aligned(16))) uint32_t img_all[4][kImg64U32];
@@ -387,8 +388,8 @@ __global__ __launch_bounds__(256) void k_enc128v64_write(const uint64_t * __rest
     if (!R.init(in, nunits, wv))
         return;
     const uint64_t stv = D1 ? R.start_lane(in, starts, start0, t) : 0ull;
-    const uint64_t ov = t < R.n ? off[R.first + t] : 0ull;
-    const uint64_t ev = t < R.n ? off[R.first + t + 1u] : 0ull;
+    uint64_t ov, ev;
+    run_offsets(off, R.first, R.n, run_base(run_pre, run_tile, R.first / kEnc64Run), t, ov, ev);
     const uint64_t pwv = t < R.n ? plan[R.first + t] : 0ull;
     const uint64_t out_base = reinterpret_cast<uint64_t>(out);
     const uint64_t cap_end = out_base + out_cap;
@@ -424,10 +425,7 @@ namespace tpf
 
 size_t enc128v64_workspace(uint64_t nunits)
 {
-    size_t scan_bytes = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, static_cast<uint64_t *>(nullptr),
-                                           static_cast<int>(std::min<uint64_t>(nunits + 1, 0x7FFFFFFF)));
-    return ((nunits * 8u + 255u) & ~size_t(255)) + scan_bytes + 256;
+    return ((nunits * 8u + 255u) & ~size_t(255)) + RunScanWs<uint64_t>::bytes((nunits + dev::kEnc64Run - 1u) / dev::kEnc64Run);
 }
 
 namespace
@@ -436,21 +434,23 @@ template <uint32_t NB, bool D1>
 hipError_t enc64_launch(const uint64_t * in, uint64_t nunits, const uint64_t * starts, uint64_t start0, uint8_t * out,
                         uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t s)
 {
+    if (ws_bytes < enc128v64_workspace(nunits))
+        return hipErrorInvalidValue;
     auto * plan = static_cast<uint64_t *>(ws);
     const size_t plan_bytes = (nunits * 8u + 255u) & ~size_t(255);
-    void * scan_tmp = static_cast<uint8_t *>(ws) + plan_bytes;
-    size_t scan_bytes = ws_bytes > plan_bytes ? ws_bytes - plan_bytes : 0;
+    const uint64_t nruns = (nunits + dev::kEnc64Run - 1u) / dev::kEnc64Run;
+    const RunScanWs<uint64_t> rs = RunScanWs<uint64_t>::carve(static_cast<uint8_t *>(ws) + plan_bytes, nruns);
     const uint64_t per_wg = 4ull * dev::kEnc64Run;
     const uint32_t grid = static_cast<uint32_t>((nunits + per_wg - 1) / per_wg);
-    hipLaunchKernelGGL((dev::k_enc128v64_plan<NB, D1>), dim3(grid), dim3(256), 0, s, in, nunits, starts, start0, off, plan);
+    hipLaunchKernelGGL((dev::k_enc128v64_plan<NB, D1>), dim3(grid), dim3(256), 0, s, in, nunits, starts, start0, off, plan, rs.tot);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return e;
-    e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, off, static_cast<int>(nunits + 1), s);
+    e = launch_run_scan_u64(rs.tot, nruns, rs.pre, rs.tile, off + nunits, s);
     if (e != hipSuccess)
         return e;
-    hipLaunchKernelGGL((dev::k_enc128v64_write<NB, D1>), dim3(grid), dim3(256), 0, s, in, nunits, starts, start0, off, plan, out,
-                       out_cap);
+    hipLaunchKernelGGL((dev::k_enc128v64_write<NB, D1>), dim3(grid), dim3(256), 0, s, in, nunits, starts, start0, off, plan, rs.pre,
+                       rs.tile, out, out_cap);
     return hipGetLastError();
 }
 } // namespace

@@ -8,7 +8,7 @@
 // is the same three-pass scheme as the 256v32 encoder: plan pass -> exclusive
 // scan -> write pass (LDS image copied out with dword stores and byte stores
 // on the two shared edge dwords).
-#include <hipcub/hipcub.hpp>
+#include "p4_scan.h"
 
 #include "p4_dec_run.h"
 #include "p4_generic.h"
@@ -177,11 +177,14 @@ struct Unit4
     T v[4];
 };
 
+// Plan pass (!WRITE): sizes into off[unit] and one byte total per wave run
+// (run_tot); write pass: offsets rebuilt from the run scan (p4_scan.h).
 template <Fmt F, bool D1, bool WRITE, uint32_t NC = 3>
 __global__ __launch_bounds__(256) void k_enc_gr(const typename FmtTraits<F>::T * __restrict in, uint64_t nblocks, uint32_t n,
                                                  const typename FmtTraits<F>::T * __restrict starts,
                                                  typename FmtTraits<F>::T start0, uint64_t * __restrict off,
-                                                 uint8_t * __restrict out, uint64_t out_cap)
+                                                 uint32_t * __restrict run_tot, const uint64_t * __restrict run_pre,
+                                                 const uint64_t * __restrict run_tile, uint8_t * __restrict out, uint64_t out_cap)
 {
     using G = UnitGeom<F, false>;
     using T = typename FmtTraits<F>::T;
@@ -189,9 +192,6 @@ __global__ __launch_bounds__(256) void k_enc_gr(const typename FmtTraits<F>::T *
     __shared__ __attribute__((aligned(16))) uint32_t hist[4][kPlanGHistU32];
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
-    if constexpr (!WRITE)
-        if (blockIdx.x == 0 && threadIdx.x == 0)
-            off[nblocks] = 0; // exclusive scan over nblocks+1 entries yields the total
     EncRunG<F> R;
     if (!R.init(in, nblocks, wv, n))
         return;
@@ -200,8 +200,8 @@ __global__ __launch_bounds__(256) void k_enc_gr(const typename FmtTraits<F>::T *
     uint32_t olo = 0u, ohi = 0u;
     if constexpr (WRITE)
     {
-        const uint64_t ov = t < R.nr ? off[R.first + t] : 0ull;
-        const uint64_t ev = t < R.nr ? off[R.first + t + 1u] : 0ull;
+        uint64_t ov, ev;
+        run_offsets(off, R.first, R.nr, run_base(run_pre, run_tile, R.first / kGRun), t, ov, ev);
         szv = static_cast<uint32_t>(ev - ov);
         olo = static_cast<uint32_t>(ov);
         ohi = static_cast<uint32_t>(ov >> 32);
@@ -289,8 +289,11 @@ __global__ __launch_bounds__(256) void k_enc_gr(const typename FmtTraits<F>::T *
         }
     }
     if constexpr (!WRITE)
+    {
         if (t < R.nr)
             off[R.first + t] = szv;
+        publish_run_total(run_tot, R.first / kGRun, t < R.nr ? szv : 0u, t);
+    }
 }
 
 } // namespace tpf::dev
@@ -326,17 +329,20 @@ hipError_t enc_fmt_d(const void * in, uint64_t nblocks, uint32_t n, const void *
     const T * sp = static_cast<const T *>(starts);
     const uint64_t per_wg = 4ull * dev::kGRun;
     const uint32_t g = static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg);
-    hipLaunchKernelGGL((dev::k_enc_gr<F, D1, false>), dim3(g), dim3(256), 0, s, ip, nblocks, n, sp, static_cast<T>(start0), off, out,
-                       out_cap);
+    const uint64_t nruns = (nblocks + dev::kGRun - 1u) / dev::kGRun;
+    if (ws_bytes < RunScanWs<uint64_t>::bytes(nruns))
+        return hipErrorInvalidValue;
+    const RunScanWs<uint64_t> rs = RunScanWs<uint64_t>::carve(ws, nruns);
+    hipLaunchKernelGGL((dev::k_enc_gr<F, D1, false>), dim3(g), dim3(256), 0, s, ip, nblocks, n, sp, static_cast<T>(start0), off, rs.tot,
+                       nullptr, nullptr, out, out_cap);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return e;
-    size_t sb = ws_bytes;
-    e = hipcub::DeviceScan::ExclusiveSum(ws, sb, off, static_cast<int>(nblocks + 1), s);
+    e = launch_run_scan_u64(rs.tot, nruns, rs.pre, rs.tile, off + nblocks, s);
     if (e != hipSuccess)
         return e;
-    hipLaunchKernelGGL((dev::k_enc_gr<F, D1, true>), dim3(g), dim3(256), 0, s, ip, nblocks, n, sp, static_cast<T>(start0), off, out,
-                       out_cap);
+    hipLaunchKernelGGL((dev::k_enc_gr<F, D1, true>), dim3(g), dim3(256), 0, s, ip, nblocks, n, sp, static_cast<T>(start0), off, nullptr,
+                       rs.pre, rs.tile, out, out_cap);
     return hipGetLastError();
 }
 
@@ -350,13 +356,7 @@ hipError_t enc_fmt(const void * in, uint64_t nblocks, uint32_t n, bool d1, const
 
 } // namespace
 
-size_t generic_workspace(uint64_t nblocks)
-{
-    size_t scan_bytes = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, static_cast<uint64_t *>(nullptr),
-                                     static_cast<int>(std::min<uint64_t>(nblocks + 1, 0x7FFFFFFF)));
-    return scan_bytes + 256;
-}
+size_t generic_workspace(uint64_t nblocks) { return RunScanWs<uint64_t>::bytes((nblocks + dev::kGRun - 1u) / dev::kGRun); }
 
 hipError_t launch_dec_generic(int fmt, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t n,
                               void * out, const void * starts, unsigned long long * err, hipStream_t s)

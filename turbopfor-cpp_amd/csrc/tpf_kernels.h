@@ -52,10 +52,10 @@ hipError_t launch_probe256v32(const uint8_t * in, uint64_t in_bytes, const uint6
                               hipStream_t stream);
 
 size_t d1chain_workspace(uint64_t nblocks);
-hipError_t launch_d1chain_sums(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * incl,
-                               void * ws, size_t ws_bytes, unsigned long long * err, hipStream_t stream);
+hipError_t launch_d1chain_sums(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, void * ws, size_t ws_bytes,
+                               uint32_t * total, unsigned long long * err, hipStream_t stream);
 hipError_t launch_d1chain_decode(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * out,
-                                 const uint32_t * incl, uint32_t base, unsigned long long * err, hipStream_t stream);
+                                 const void * ws, uint32_t base, unsigned long long * err, hipStream_t stream);
 
 hipError_t launch_dec128v64(uint32_t nb, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nunits,
                             uint64_t * out, const uint64_t * starts, unsigned long long * err, hipStream_t s);
