@@ -724,7 +724,7 @@ def run_c3(args, world, rank, dev, T, chained):
             "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             **traffic_fields("c3chain" if chained else "c3", nb),
             "kernel_ms_avg": round(avg_ms, 4),
-            "kernel": ("k_dec256v32w<SumOnly> + hipcub scan + k_dec256v32w<Prefix>" if chained
+            "kernel": ("k_dec256v32w<SumOnly> + run scan (2 small kernels) + k_dec256v32w<Prefix>" if chained
                        else "tpf::dev::k_dec256v32w<StartMode::PerBlock>"),
             "probe_GBps": round(probe_alg / (float(np.mean(probe_ms)) * 1e-3) / 1e9, 1),
             "ms_vs_probe": round(avg_ms / float(np.mean(probe_ms)), 3),
@@ -808,7 +808,7 @@ def run_c4(args, world, rank, dev, T):
     rt_gbs = gbs(alg_enc + alg_dec, rt_ms)
     roof = {"bound": "hbm", "achieved": rt_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(rt_gbs / HBM_PEAK_GBS, 4), **traffic_fields("c4", nb),
-            "kernel": "round-trip step: k_enc256v32_plan + rocprim offset scan + k_enc256v32_write + k_dec256v32w<None>",
+            "kernel": "round-trip step: k_enc256v32_plan + run scan (2 small kernels) + k_enc256v32_write + k_dec256v32w<None>",
             "kernel_ms_avg": round(float(np.mean(rt_ms)), 4), "alg_bytes_per_launch": int(alg_enc + alg_dec),
             "alg_bytes_def": "encode: 1024 B values + block bytes + 8 B offset; decode: block bytes + 1024 B + 8 B",
             "enc_achieved_GBps": gbs(alg_enc, enc_ms), "enc_ms_avg": round(float(np.mean(enc_ms)), 4),
