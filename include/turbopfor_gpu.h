@@ -59,6 +59,13 @@ int tpf_probe256v32(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_of
  * write `bytes` to d_dst, 2 = copy `bytes` from d_src to d_dst; 16-byte
  * lanes, non-temporal, grid-stride.  bytes is rounded down to 16. */
 int tpf_probe_hbm(int kind, void *d_dst, const void *d_src, uint64_t bytes, void *stream);
+/* Test hook (no product use): the run scan every two-pass kernel pair uses
+ * between its passes (p4_scan.h).  d_tot: nruns u32 totals; writes
+ * d_base[r] = sum of d_tot[0..r) (u64, exclusive) and *d_total = the sum of
+ * all.  d_ws: tpf_test_run_scan_workspace_size(nruns) bytes. */
+size_t tpf_test_run_scan_workspace_size(uint64_t nruns);
+int tpf_test_run_scan(const uint32_t *d_tot, uint64_t nruns, uint64_t *d_base, uint64_t *d_total, void *d_ws, size_t ws_bytes,
+                      void *stream);
 
 /* Replaces turbopfor::p4D1Dec256v32 (include/turbopfor.h:42, dispatch.cpp:97-104):
  * block i is decoded with start d_starts[i] (the value preceding the block). */

@@ -117,6 +117,19 @@ int tpf_probe_hbm(int kind, void * d_dst, const void * d_src, uint64_t bytes, vo
     return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_probe_hbm");
 }
 
+size_t tpf_test_run_scan_workspace_size(uint64_t nruns) { return tpf::test_run_scan_workspace(nruns); }
+
+int tpf_test_run_scan(const uint32_t * d_tot, uint64_t nruns, uint64_t * d_base, uint64_t * d_total, void * d_ws, size_t ws_bytes,
+                      void * stream)
+{
+    if (int rc = check_device())
+        return rc;
+    if (!d_total || (nruns && (!d_tot || !d_base || !d_ws)))
+        return fail(TPF_EINVAL, "tpf_test_run_scan: null pointer");
+    hipError_t e = tpf::test_run_scan(d_tot, nruns, d_base, d_total, d_ws, ws_bytes, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_test_run_scan");
+}
+
 int tpf_p4d1dec256v32_batch(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nblocks, uint32_t * d_out,
                             const uint32_t * d_starts, uint64_t * d_err, void * stream)
 {

@@ -89,6 +89,15 @@ __global__ __launch_bounds__(1024) void k_run_scan_tops(T * __restrict tile, uin
         *total = carry;
 }
 
+// test hook: base[r] = tile[r / kScanTile] + pre[r]
+__global__ __launch_bounds__(256) void k_run_scan_combine(const uint64_t * __restrict pre, const uint64_t * __restrict tile, uint64_t nruns,
+                                                          uint64_t * __restrict base)
+{
+    const uint64_t r = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+    if (r < nruns)
+        base[r] = run_base(pre, tile, r);
+}
+
 } // namespace tpf::dev
 
 namespace tpf
@@ -119,6 +128,24 @@ hipError_t launch_run_scan_u64(const uint32_t * tot, uint64_t nruns, uint64_t * 
 hipError_t launch_run_scan_u32(const uint32_t * tot, uint64_t nruns, uint32_t * pre, uint32_t * tile, uint32_t * total, hipStream_t s)
 {
     return run_scan<uint32_t>(tot, nruns, pre, tile, total, s);
+}
+
+size_t test_run_scan_workspace(uint64_t nruns) { return RunScanWs<uint64_t>::bytes(nruns); }
+
+hipError_t test_run_scan(const uint32_t * tot, uint64_t nruns, uint64_t * base, uint64_t * total, void * ws, size_t ws_bytes, hipStream_t s)
+{
+    if (ws_bytes < test_run_scan_workspace(nruns))
+        return hipErrorInvalidValue;
+    const RunScanWs<uint64_t> w = RunScanWs<uint64_t>::carve(ws, nruns);
+    hipError_t e = hipMemcpyAsync(w.tot, tot, 4u * nruns, hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess)
+        return e;
+    e = run_scan<uint64_t>(w.tot, nruns, w.pre, w.tile, total, s);
+    if (e != hipSuccess || nruns == 0)
+        return e;
+    hipLaunchKernelGGL(dev::k_run_scan_combine, dim3(static_cast<uint32_t>((nruns + 255u) / 256u)), dim3(256), 0, s, w.pre, w.tile, nruns,
+                       base);
+    return hipGetLastError();
 }
 
 } // namespace tpf

@@ -51,6 +51,9 @@ hipError_t launch_dec256v32(const uint8_t * in, uint64_t in_bytes, const uint64_
 hipError_t launch_probe256v32(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * out,
                               hipStream_t stream);
 
+// run scan test hook (p4_scan.hip)
+size_t test_run_scan_workspace(uint64_t nruns);
+hipError_t test_run_scan(const uint32_t * tot, uint64_t nruns, uint64_t * base, uint64_t * total, void * ws, size_t ws_bytes, hipStream_t s);
 size_t d1chain_workspace(uint64_t nblocks);
 hipError_t launch_d1chain_sums(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, void * ws, size_t ws_bytes,
                                uint32_t * total, unsigned long long * err, hipStream_t stream);
