@@ -39,7 +39,10 @@ struct UnitGeom
 constexpr uint32_t kGRun = 16;
 
 template <Fmt F, bool D1, uint32_t NC = 4>
-__global__ __launch_bounds__(256) void k_dec_gr(const uint8_t * __restrict in, uint64_t in_bytes, const uint64_t * __restrict off,
+// SGPRs capped at 80 (a few spill to VGPR lanes): at 101 the scalar file
+// (800 per SIMD, 16-register granules + 16) held the kernel to 6 waves per
+// SIMD, one below its VGPR limit; C1 decode +4-5% (A/B on one box).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void k_dec_gr(const uint8_t * __restrict in, uint64_t in_bytes, const uint64_t * __restrict off,
                                                  uint64_t nblocks, uint32_t n, typename FmtTraits<F>::T * __restrict out,
                                                  const typename FmtTraits<F>::T * __restrict starts,
                                                  unsigned long long * __restrict err)
