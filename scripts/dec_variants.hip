@@ -12,6 +12,9 @@
 //   DEAL 5: contiguous runs, workgroups remapped in chunks of 8K: XCD x
 //           takes WGs [x*K, (x+1)*K) of each chunk (XCD-contiguous pieces of
 //           K workgroups, all XCDs moving through the stream together)
+//   DEAL 13..17 (python ids): contiguous runs, output stored by a buffer store
+//           with cache-policy aux 0 (plain) / 2 (nt) / 16 (sc1) / 17 (sc0 sc1)
+//           / 18 (sc1 nt)
 // PROBE: the same loads and stores with the decoding removed.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++20 -shared -fPIC
 //        -I turbopfor-cpp_amd/csrc -o scripts/libdecvar.so scripts/dec_variants.hip
@@ -166,7 +169,7 @@ __device__ __forceinline__ uint32_t decode_block_v(const uint32_t * lds, uint32_
     return end - s;
 }
 
-template <int DEAL, bool PROBE, uint32_t kRun = 16, uint32_t K = 1, uint32_t VB = 0, uint32_t NC = 6, int MINW = 7>
+template <int DEAL, bool PROBE, uint32_t kRun = 16, uint32_t K = 1, uint32_t VB = 0, int STAUX = -1, uint32_t NC = 6, int MINW = 7>
 __global__ __launch_bounds__(256, MINW) void k_var(const VArgs A)
 {
     __shared__ uint32_t slots[4][kSlotBytes / 4];
@@ -220,19 +223,28 @@ __global__ __launch_bounds__(256, MINW) void k_var(const VArgs A)
     P.init(in_base, in_end, o, e, valid);
     uint32_t * const out_run = A.out + first * 256u;
     uint64_t badmask = 0u;
+    // STAUX >= 0: output through a buffer store with that cache-policy aux
+    // (bit 0 sc0, bit 1 nt, bit 4 sc1) instead of the product's nt store
+    const __amdgpu_buffer_rsrc_t ors = make_rsrc(out_run, n * 1024u);
+    auto store = [&](u32x4 * dst, uint32_t jj, const u32x4 & v) {
+        if constexpr (STAUX < 0)
+            st16<2>(dst, v);
+        else
+            __builtin_amdgcn_raw_buffer_store_b128(v, ors, static_cast<int>(jj * 1024u + 16u * t), 0, STAUX);
+    };
 
     auto issue = [&](Chunk & c, uint32_t jj) { P.template issue<2>(c, jj, t); };
     auto consume = [&](const Chunk & c, uint32_t jj) {
         u32x4 * dst = reinterpret_cast<u32x4 *>(out_run + jj * stride * 256u) + t;
         if constexpr (PROBE)
         {
-            st16<2>(dst, c.a | P.big_rest_or(jj, t));
+            store(dst, jj, c.a | P.big_rest_or(jj, t));
             return;
         }
         const uint32_t ctl = P.stage(c, jj, slot, t);
         u32x4 v;
         const uint32_t used = decode_block_v<VB>(slot, (ctl >> kCtlShift) & 15u, P.head(c, ctl, slot), scr, t, v);
-        st16<2>(dst, v);
+        store(dst, jj, v);
         wave_lds_sync();
         if (used != rl(P.len, jj))
             badmask |= 1ull << jj;
@@ -259,7 +271,7 @@ __global__ __launch_bounds__(256, MINW) void k_var(const VArgs A)
         atomicMin(A.err, static_cast<unsigned long long>(first + stride * __builtin_ctzll(badmask)));
 }
 
-template <int DEAL, bool PROBE, uint32_t K = 1, uint32_t VB = 0>
+template <int DEAL, bool PROBE, uint32_t K = 1, uint32_t VB = 0, int STAUX = -1>
 int launch_var(const VArgs & A0, hipStream_t s)
 {
     constexpr uint32_t kRun = DEAL == 4 ? 32u : 16u;
@@ -267,7 +279,7 @@ int launch_var(const VArgs & A0, hipStream_t s)
     const uint64_t waves = (A.nblocks + kRun - 1u) / kRun;
     A.waves = waves;
     const uint32_t grid = static_cast<uint32_t>((waves + 3u) / 4u);
-    hipLaunchKernelGGL((k_var<DEAL, PROBE, kRun, K, VB>), dim3(grid), dim3(256), 0, s, A);
+    hipLaunchKernelGGL((k_var<DEAL, PROBE, kRun, K, VB, STAUX>), dim3(grid), dim3(256), 0, s, A);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -306,6 +318,16 @@ extern "C" int decvar_launch(int deal, int probe, const void * in, uint64_t in_b
         case 20: return launch_var<0, false, 1, 1>(A, s);
         case 22: return launch_var<0, false, 1, 2>(A, s);
         case 24: return launch_var<0, false, 1, 3>(A, s);
+        case 26: return launch_var<0, false, 1, 0, 0>(A, s);
+        case 27: return launch_var<0, true, 1, 0, 0>(A, s);
+        case 28: return launch_var<0, false, 1, 0, 2>(A, s);
+        case 29: return launch_var<0, true, 1, 0, 2>(A, s);
+        case 30: return launch_var<0, false, 1, 0, 16>(A, s);
+        case 31: return launch_var<0, true, 1, 0, 16>(A, s);
+        case 32: return launch_var<0, false, 1, 0, 17>(A, s);
+        case 33: return launch_var<0, true, 1, 0, 17>(A, s);
+        case 34: return launch_var<0, false, 1, 0, 18>(A, s);
+        case 35: return launch_var<0, true, 1, 0, 18>(A, s);
         default: return -2;
     }
 }

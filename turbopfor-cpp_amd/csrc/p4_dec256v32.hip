@@ -92,6 +92,16 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
     }
     uint32_t sumv = 0u;
     uint32_t * const out_run = SM == StartMode::SumOnly ? nullptr : A.out + first * 256u;
+    // POL bit 3: the run's output through one buffer descriptor, stored
+    // "sc1 nt" (streamed and not kept in the XCD's L2): 1-2.5% over nt alone
+    // on every stream shape (scripts/dec_variants.hip)
+    const __amdgpu_buffer_rsrc_t ors = make_rsrc(out_run, (POL & 8u) && out_run ? n * stride * 1024u : 0u);
+    auto put = [&](uint32_t jj, const u32x4 & v) {
+        if constexpr ((POL & 8u) != 0u)
+            st16_run(ors, jj * stride * 1024u + 16u * t, v);
+        else
+            st16<POL>(reinterpret_cast<u32x4 *>(out_run + jj * stride * 256u) + t, v);
+    };
     uint64_t badmask = 0u;
     constexpr bool sum_pass = SM == StartMode::SumOnly;
 
@@ -99,8 +109,7 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
     auto consume = [&](const Chunk & c, uint32_t jj) {
         if constexpr (SM == StartMode::Probe)
         {
-            st16<POL>(reinterpret_cast<u32x4 *>(out_run + jj * stride * 256u) + t,
-                      ONE ? (c.a | P.big_rest_or(jj, t)) : (c.a | c.b));
+            put(jj, ONE ? (c.a | P.big_rest_or(jj, t)) : (c.a | c.b));
             return;
         }
         const uint32_t ctl = P.stage(c, jj, slot, t);
@@ -116,7 +125,7 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
             used = decode_block256v32(slot, (ctl >> kCtlShift) & 15u, P.head(c, ctl, slot), scr, t, v);
             if constexpr (SM == StartMode::PerBlock || SM == StartMode::Prefix)
                 apply_delta1_256(v, rl(startv, jj));
-            st16<POL>(reinterpret_cast<u32x4 *>(out_run + jj * stride * 256u) + t, v);
+            put(jj, v);
         }
         wave_lds_sync();
         if (used != rl(P.len, jj))
@@ -163,8 +172,9 @@ namespace tpf
 
 namespace
 {
-// The measured best of round 1's A/B knobs, fixed (no environment switch on
-// the product path): non-temporal output stores, contiguous runs (POL 2),
+// The measured best of the A/B knobs, fixed (no environment switch on the
+// product path): "sc1 nt" output stores through a run descriptor (POL 8,
+// round 2; non-temporal alone was POL 2), contiguous runs,
 // one 16-byte load per lane per block with six blocks in flight (ONE / NC 6),
 // 7 waves per SIMD.  (C2 899 -> 906, C3 1080 -> 1106 G int32/s vs two loads
 // per block with three in flight)
@@ -173,7 +183,7 @@ hipError_t launch_mode(const dev::DecArgs & A, hipStream_t stream)
 {
     constexpr uint64_t per_wg = 4ull * dev::kRunDefault;
     const uint32_t grid = static_cast<uint32_t>((A.nblocks + per_wg - 1) / per_wg);
-    hipLaunchKernelGGL((dev::k_dec256v32w<SM, dev::kRunDefault, 2, 6, 7, true>), dim3(grid), dim3(256), 0, stream, A);
+    hipLaunchKernelGGL((dev::k_dec256v32w<SM, dev::kRunDefault, 2 | 8, 6, 7, true>), dim3(grid), dim3(256), 0, stream, A);
     return hipGetLastError();
 }
 } // namespace

@@ -29,11 +29,19 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane)
 }
 
 // POL (A/B knob): bit 0 = non-temporal loads (measured -4%), bit 1 =
-// non-temporal stores (measured +2.5%, default), bit 2 = block order.
+// non-temporal stores (measured +2.5%), bit 2 = block order, bit 3 = "sc1 nt"
+// stores through a run descriptor (round 2: +1-2.5% over bit 1, default).
 template <uint32_t POL>
 __device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t off)
 {
     return __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), 0, (POL & 1u) ? 2 : 0);
+}
+
+// 16-byte store through a buffer descriptor with cache policy "sc1 nt"
+// (aux: bit 1 nt, bit 4 sc1): streamed output that is not kept in the XCD's L2
+__device__ __forceinline__ void st16_run(__amdgpu_buffer_rsrc_t r, uint32_t off, const u32x4 & v)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, static_cast<int>(off), 0, 18);
 }
 
 template <uint32_t POL>
