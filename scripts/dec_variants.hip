@@ -14,7 +14,7 @@
 //           K workgroups, all XCDs moving through the stream together)
 //   DEAL 13..17 (python ids): contiguous runs, output stored by a buffer store
 //           with cache-policy aux 0 (plain) / 2 (nt) / 16 (sc1) / 17 (sc0 sc1)
-//           / 18 (sc1 nt)
+//           / 18 (sc1 nt); 18, 19: 3 (sc0 nt) / 19 (sc0 sc1 nt)
 // PROBE: the same loads and stores with the decoding removed.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++20 -shared -fPIC
 //        -I turbopfor-cpp_amd/csrc -o scripts/libdecvar.so scripts/dec_variants.hip
@@ -328,6 +328,10 @@ extern "C" int decvar_launch(int deal, int probe, const void * in, uint64_t in_b
         case 33: return launch_var<0, true, 1, 0, 17>(A, s);
         case 34: return launch_var<0, false, 1, 0, 18>(A, s);
         case 35: return launch_var<0, true, 1, 0, 18>(A, s);
+        case 36: return launch_var<0, false, 1, 0, 3>(A, s);
+        case 37: return launch_var<0, true, 1, 0, 3>(A, s);
+        case 38: return launch_var<0, false, 1, 0, 19>(A, s);
+        case 39: return launch_var<0, true, 1, 0, 19>(A, s);
         default: return -2;
     }
 }
