@@ -283,6 +283,18 @@ int launch_var(const VArgs & A0, hipStream_t s)
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// sc1 nt stores with another pipeline depth / occupancy
+template <uint32_t NC, int MINW, bool PROBE>
+int launch_nc(const VArgs & A0, hipStream_t s)
+{
+    VArgs A = A0;
+    const uint64_t waves = (A.nblocks + 15u) / 16u;
+    A.waves = waves;
+    const uint32_t grid = static_cast<uint32_t>((waves + 3u) / 4u);
+    hipLaunchKernelGGL((k_var<0, PROBE, 16, 1, 0, 18, NC, MINW>), dim3(grid), dim3(256), 0, s, A);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 } // namespace tpf::dev
 
 extern "C" int decvar_launch(int deal, int probe, const void * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, void * out,
@@ -332,6 +344,10 @@ extern "C" int decvar_launch(int deal, int probe, const void * in, uint64_t in_b
         case 37: return launch_var<0, true, 1, 0, 3>(A, s);
         case 38: return launch_var<0, false, 1, 0, 19>(A, s);
         case 39: return launch_var<0, true, 1, 0, 19>(A, s);
+        case 40: return launch_nc<4, 8, false>(A, s);
+        case 41: return launch_nc<4, 8, true>(A, s);
+        case 42: return launch_nc<5, 8, false>(A, s);
+        case 43: return launch_nc<5, 8, true>(A, s);
         default: return -2;
     }
 }
