@@ -59,6 +59,23 @@ def test_no_cpu_fallback_without_device(lib):
     assert lib.tpf_p4Dec256v32(buf, 256, out) is None
 
 
+def test_perblock_mode_query_and_set(lib):
+    """tpf_perblock_mode: < 0 queries, 0/1/2 select a design, anything else
+    means the default (0); each call returns the previous mode.  No server
+    exists on a machine without a device, so the switch touches no GPU."""
+    lib.tpf_perblock_mode.restype = ctypes.c_int
+    lib.tpf_perblock_mode.argtypes = [ctypes.c_int]
+    prev = lib.tpf_perblock_mode(-1)
+    try:
+        assert lib.tpf_perblock_mode(2) == prev
+        assert lib.tpf_perblock_mode(-1) == 2
+        assert lib.tpf_perblock_mode(1) == 2
+        assert lib.tpf_perblock_mode(7) == 1
+        assert lib.tpf_perblock_mode(-5) == 0
+    finally:
+        lib.tpf_perblock_mode(prev)
+
+
 @pytest.mark.parametrize("fname,fmt", [("g32.bin", "32"), ("g128v32.bin", "128v32"), ("g256v32.bin", "256v32"),
                                        ("g128v64.bin", "128v64"), ("g256v64.bin", "256v64")])
 def test_framing_matches_golden(lib, fname, fmt):
