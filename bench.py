@@ -516,17 +516,30 @@ def line(metric, value, unit, world, steps, warmup, elapsed, dtype, data, config
 
 
 # ---------------------------------------------------------------- workloads
-def run_c2(args, world, rank, dev, T):
+def gen_c5(nblocks, exc_pct, seed, dev):
+    """C5 shard (SURVEY.md 8 d: 80M blocks as 8 x 10M shards, bw 8 and 16 at
+    10% exceptions): the first half of the shard's blocks bw 8, the rest bw 16."""
+    h = nblocks // 2
+    vals = torch.empty((nblocks, 256), dtype=torch.int32, device=dev)
+    vals[:h] = gen_bw(h, 8, exc_pct, seed, dev)
+    vals[h:] = gen_bw(nblocks - h, 16, exc_pct, seed, dev)
+    return vals
+
+
+def run_c2(args, world, rank, dev, T, c5=False):
     nb = args.nblocks
     t0 = time.time()
-    vals, seg = gen_c2(nb, args.exc, seed=42 + rank, dev=dev)
+    if c5:
+        vals = gen_c5(nb, args.exc, seed=42 + rank, dev=dev)
+    else:
+        vals, seg = gen_c2(nb, args.exc, seed=42 + rank, dev=dev)
     packed_full, offs = tpf.enc256v32(vals)
     packed = packed_full.clone()
     del packed_full
     torch.cuda.synchronize()
     pbytes = packed.numel()
     if rank == 0:
-        log(f"[bench] c2: {nb} blocks generated+encoded in {time.time() - t0:.1f}s, packed {pbytes / 1e9:.3f} GB "
+        log(f"[bench] {'c5' if c5 else 'c2'}: {nb} blocks generated+encoded in {time.time() - t0:.1f}s, packed {pbytes / 1e9:.3f} GB "
             f"({pbytes / nb:.1f} B/block)")
     out = torch.empty((nb, 256), dtype=torch.int32, device=dev)
     err = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -555,7 +568,7 @@ def run_c2(args, world, rank, dev, T):
         return None
     probe = alg / (float(np.mean(probe_ms)) * 1e-3) / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), **traffic_fields("c2", nb),
+            "frac": round(achieved / HBM_PEAK_GBS, 4), **traffic_fields("c5" if c5 else "c2", nb),
             "kernel": "tpf::dev::k_dec256v32w<StartMode::None>", "kernel_ms_avg": round(avg_ms, 4),
             "kernel_ms_median": round(float(np.median(kern_ms)), 4), "kernel_ms_min": round(float(np.min(kern_ms)), 4),
             "alg_bytes_per_launch": int(alg),
@@ -567,14 +580,16 @@ def run_c2(args, world, rank, dev, T):
     cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(packed.cpu().numpy(),
                                                                           offs.cpu().numpy().astype(np.uint64), nb)
     value = nb * 256 * world / (elapsed / args.steps) / 1e9
-    cfg = {"workload": "C2: p4Dec256v32, 10M blocks x 256 u32 per GPU, bw 1..32 sweep (32 equal segments), "
-                       "10% exceptions for bw<=28",
+    cfg = {"workload": ("C5: p4Dec256v32 sharded, 10M blocks x 256 u32 per GPU (80M at 8 GPUs), half bw 8 / half "
+                        "bw 16, 10% exceptions" if c5 else
+                        "C2: p4Dec256v32, 10M blocks x 256 u32 per GPU, bw 1..32 sweep (32 equal segments), "
+                        "10% exceptions for bw<=28"),
            "nblocks_per_gpu": nb, "packed_bytes_per_gpu": pbytes, "bytes_per_block": round(pbytes / nb, 1),
            "compressed_GBps": round(pbytes * world / (elapsed / args.steps) / 1e9, 1),
            "parallelism": f"shard{world}", "verified": ok}
     if e2e:
         cfg["e2e_host_pinned"] = e2e
-    data = ("synthetic (GPU-generated C2 values, GPU-encoded; full-size decode verified bit-exact: "
+    data = (f"synthetic (GPU-generated {'C5' if c5 else 'C2'} values, GPU-encoded; full-size decode verified bit-exact: "
             + ("ok" if ok else "MISMATCH") + ")")
     return line(METRIC, value, "G int32/s", world, args.steps, args.warmup, elapsed, "u32", data, cfg, roof, cpu), ok
 
@@ -929,7 +944,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--nblocks", type=int, default=10_000_000, help="blocks per GPU (shard)")
     ap.add_argument("--exc", type=float, default=10.0)
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c3chain", "c4", "sweep"])
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c3chain", "c4", "c5", "sweep"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="c2: also measure the pinned host-memory path")
     ap.add_argument("--no-probes", action="store_true", help="c2: skip the in-run HBM read/write/copy probes")
@@ -974,6 +989,8 @@ def main():
         res = run_c1(args, world, rank, dev, T)
     elif args.workload == "c2":
         res = run_c2(args, world, rank, dev, T)
+    elif args.workload == "c5":
+        res = run_c2(args, world, rank, dev, T, c5=True)
     elif args.workload == "c3":
         res = run_c3(args, world, rank, dev, T, chained=False)
     elif args.workload == "c3chain":
