@@ -1,6 +1,8 @@
 """A/B of the 256v32 encoders on one box (C4 mix, 10M blocks): the production
-single-launch pipelined encoder vs the two-pass one (tpf_probe_enc256v32 mode
-3), alternating, HIP events on the launch stream; both outputs verified."""
+two-pass encoder (batch entry and tpf_probe_enc256v32 mode 3) vs the rejected
+single-pass look-back encoder's variants (modes 4-12), alternating, HIP events on
+the launch stream; every output verified.  ENC_AB_PIPE=1 adds the rejected
+pipelined encoder's variants (modes >= 16)."""
 import ctypes
 import os
 import sys
@@ -42,10 +44,13 @@ def pv(ci, lag, minw, k):
     return probe(16 + ci + 1024 * lag + 65536 * minw + (1 << 20) * k)
 
 
-VARIANTS = [("twopass", twopass), ("pipe", pipe)] + [
-    (f"ci{ci}_lag{lag}_w{w}_k{k}", pv(ci, lag, w, k))
-    for ci, lag, w, k in [(256, 2, 8, 8), (256, 2, 0, 8), (256, 2, 6, 8), (256, 2, 8, 16), (256, 4, 8, 8),
-                          (512, 2, 0, 8), (128, 4, 0, 8)]]
+VARIANTS = [("twopass", twopass), ("production", pipe), ("lookback", probe(12)), ("lb_k4", probe(5)), ("lb_k6", probe(6)), ("lb_k8", probe(7)),
+            ("lb_k8_a5120", probe(8)), ("lb_k8_a4096", probe(9)), ("lb_k6_a3840", probe(10)), ("lb_k12_a7680", probe(11)),
+            ("lb_fallback", probe(4))]
+if os.environ.get("ENC_AB_PIPE"):
+    VARIANTS += [(f"ci{ci}_lag{lag}_w{w}_k{k}", pv(ci, lag, w, k))
+                 for ci, lag, w, k in [(256, 2, 8, 8), (256, 2, 0, 8), (256, 2, 6, 8), (256, 2, 8, 16), (256, 4, 8, 8),
+                                       (512, 2, 0, 8), (128, 4, 0, 8)]]
 
 
 def timed(fn, reps=10):

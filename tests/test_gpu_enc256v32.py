@@ -127,3 +127,32 @@ def test_full_size_c3_sample_vs_oracle():
     assert torch.equal(out[idx_t], vals[idx_t])
     out2 = tpf.dec256v32_chained(packed, offs, nb, start0=int(starts[0].item()) & 0xFFFFFFFF)
     assert torch.equal(out2, vals)
+
+
+@pytest.mark.parametrize("mode", [0, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
+@pytest.mark.parametrize("nb", [1, 31, 33, 1000, 20_000])
+def test_encoder_variants_vs_oracle(mode, nb):
+    """Every 256v32 encoder: 0 = production (two-pass), 3 = the two-pass
+    encoder through the probe entry, and the rejected single-pass look-back
+    encoder: 4 = forced onto its gated two-pass fallback
+    (abort raised before the launch), 5/6/7 = 4/6/8 blocks per wave in fixed
+    slots, 8-11 = per-wave arenas (blocks that do not fit are deferred), 12 =
+    its default arena.  Byte-exact vs the oracle, ragged last tiles and
+    (20,000 blocks = 625+ tiles) look-backs longer than one 256-tile poll."""
+    rng = np.random.default_rng(nb + mode)
+    bws = rng.integers(1, 33, nb)
+    blocks = np.concatenate([datagen.c2_blocks(1, int(bw), int(rng.choice([0, 5, 10, 25])), seed=int(i))
+                             for i, bw in enumerate(bws)]) if nb <= 1000 else \
+        np.concatenate([datagen.c2_blocks(nb // 32, bw, 10, seed=bw) for bw in range(1, 33)])[:nb]
+    exp_packed, exp_off = oracle_lib.enc256v32_batch(blocks)
+    vals = dev_u32(blocks)
+    if mode == 0:
+        packed, offs = tpf.enc256v32(vals)
+        packed = packed.cpu().numpy()
+    else:
+        cap = int(tpf.lib().tpf_p4enc256v32_bound(nb))
+        out = torch.zeros(cap, dtype=torch.uint8, device=DEV)
+        offs = tpf.probe_enc256v32(mode, vals, out)
+        packed = out.cpu().numpy()[:int(offs[-1].item())]
+    np.testing.assert_array_equal(offs.cpu().numpy().astype(np.uint64), exp_off)
+    np.testing.assert_array_equal(packed, exp_packed)

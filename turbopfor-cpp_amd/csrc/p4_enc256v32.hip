@@ -204,26 +204,40 @@ __device__ __forceinline__ void write_run(const EncRun & R, const uint32_t * in,
 // The plan pass leaves each block's size in off[block] and one total per
 // wave run; p4_scan.h scans only the run totals; the write pass rebuilds the
 // offsets of its run from the run base and its sizes and writes them back.
+// gate (optional): the kernels run only if *gate != 0 -- the fallback of the
+// look-back encoder below, enqueued behind it on every call and left at once
+// unless that launch aborted.  Workgroups walk their runs grid-stride, so the
+// gated launches can use a small grid.
+__device__ __forceinline__ bool gated_off(const uint32_t * gate)
+{
+    return gate != nullptr && __hip_atomic_load(const_cast<uint32_t *>(gate), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+}
+
 template <bool D1, int PROBE = 0>
 __global__ __launch_bounds__(256) void k_enc256v32_plan(const uint32_t * __restrict in, uint64_t nblocks,
                                                          const uint32_t * __restrict starts, uint32_t start0,
                                                          uint64_t * __restrict sizes, uint32_t * __restrict plan,
-                                                         uint32_t * __restrict run_tot)
+                                                         uint32_t * __restrict run_tot, const uint32_t * gate)
 {
     __shared__ __attribute__((aligned(16))) uint32_t hist[4][kPlanHistU32];
+    if (gated_off(gate))
+        return;
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
-    EncRun R;
-    if (!R.init(in, nblocks, wv))
-        return;
-    uint32_t szv, pwv; // lane j: block first+j
-    plan_run<D1, PROBE>(R, in, starts, start0, hist[wv], t, szv, pwv);
-    if (t < R.n)
+    for (uint64_t g = blockIdx.x;; g += gridDim.x)
     {
-        sizes[R.first + t] = szv;
-        plan[R.first + t] = pwv;
+        EncRun R;
+        if (!R.init_at(in, nblocks, (g * 4u + wv) * kEncRun, kEncRun))
+            return;
+        uint32_t szv, pwv; // lane j: block first+j
+        plan_run<D1, PROBE>(R, in, starts, start0, hist[wv], t, szv, pwv);
+        if (t < R.n)
+        {
+            sizes[R.first + t] = szv;
+            plan[R.first + t] = pwv;
+        }
+        publish_run_total(run_tot, R.first / kEncRun, t < R.n ? szv : 0u, t);
     }
-    publish_run_total(run_tot, R.first / kEncRun, t < R.n ? szv : 0u, t);
 }
 
 template <bool D1, int PROBE = 0>
@@ -231,26 +245,246 @@ __global__ __launch_bounds__(256) void k_enc256v32_write(const uint32_t * __rest
                                                           const uint32_t * __restrict starts, uint32_t start0,
                                                           uint64_t * __restrict off, const uint32_t * __restrict plan,
                                                           const uint64_t * __restrict run_pre, const uint64_t * __restrict run_tile,
-                                                          uint8_t * __restrict out, uint64_t out_cap)
+                                                          uint8_t * __restrict out, uint64_t out_cap, const uint32_t * gate)
 {
     __shared__ __attribute__((aligned(16))) uint32_t img_all[4][kImgU32];
     __shared__ __attribute__((aligned(16))) uint32_t val_all[4][kEncValU32];
+    if (gated_off(gate))
+        return;
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
     uint32_t * img = img_all[wv];
-    EncRun R;
-    if (!R.init(in, nblocks, wv))
-        return;
-    // lane j: destination offset (64-bit), size and plan of block first+j
-    uint64_t ov, ev;
-    run_offsets(off, R.first, R.n, run_base(run_pre, run_tile, R.first / kEncRun), t, ov, ev);
-    const uint32_t szv = static_cast<uint32_t>(ev - ov);
-    const uint32_t pwv = t < R.n ? plan[R.first + t] : 0u;
     zero_image(img, kImgU32 / 4u, t);
     wave_lds_sync();
     const uint64_t out_base = reinterpret_cast<uint64_t>(out);
-    write_run<D1, PROBE>(R, in, starts, start0, szv, pwv, static_cast<uint32_t>(ov), static_cast<uint32_t>(ov >> 32), img,
-                         val_all[wv], out_base, out_base + out_cap, t);
+    for (uint64_t g = blockIdx.x;; g += gridDim.x)
+    {
+        EncRun R;
+        if (!R.init_at(in, nblocks, (g * 4u + wv) * kEncRun, kEncRun))
+            return;
+        // lane j: destination offset (64-bit), size and plan of block first+j
+        uint64_t ov, ev;
+        run_offsets(off, R.first, R.n, run_base(run_pre, run_tile, R.first / kEncRun), t, ov, ev);
+        const uint32_t szv = static_cast<uint32_t>(ev - ov);
+        const uint32_t pwv = t < R.n ? plan[R.first + t] : 0u;
+        write_run<D1, PROBE>(R, in, starts, start0, szv, pwv, static_cast<uint32_t>(ov), static_cast<uint32_t>(ov >> 32), img,
+                             val_all[wv], out_base, out_base + out_cap, t);
+    }
+}
+
+// ---- single-pass encoder: decoupled look-back over workgroup tiles -------
+// MEASURED AND REJECTED (round 2): byte-exact in every
+// variant, 7.6-9.3 ms per 10M C4 blocks against the two-pass encoder's 5.45.
+// Reachable through tpf_probe_enc256v32 modes 4-12 for re-measurement.
+// The two-pass encoder reads the values twice (plan, then write: 1.33x the
+// round trip's algorithmic bytes).  Here one workgroup = one tile of 4 x K
+// consecutive blocks, and the values are read once:
+//   1. each wave walks its K blocks (3 in flight), plans each (p4Bits32) and
+//      builds it at once into LDS (a fixed slot per block, or packed into a
+//      per-wave arena; a block that no longer fits is deferred);
+//   2. the tile's byte total is published in status[tile] as an AGGREGATE;
+//      wave 0 then looks back over the preceding tiles' status words (256 per
+//      poll, 4 per lane): aggregates are summed down to the nearest
+//      INCLUSIVE prefix, and the tile publishes its own inclusive prefix;
+//   3. every wave writes its blocks' offsets and copies its images out, then
+//      loads and builds its deferred blocks one at a time.
+// A status word is one 8-byte {flag, value} granule written by one
+// write-through (agent-scope) store and polled with agent-scope loads, so
+// no fence orders it against anything else (MI355X_MICROARCH.md hand-offs).
+// Tiles are taken in blockIdx order: a tile waits only on lower-numbered
+// tiles, whose workgroups the dispatcher has placed first (in-order dispatch
+// within each XCD), so no residency is assumed beyond that.  Every wait is
+// bounded by the real-time clock (kLbWaitTicks): on expiry the launch raises
+// the abort word, every waiting workgroup leaves, and the gated two-pass
+// encoder enqueued behind it redoes the whole batch -- the result is the
+// same bytes either way.
+// Why it loses: the images must stay in LDS until the look-back returns, so
+// LDS caps the workgroups per CU (16-24 waves against the two passes' 32),
+// and the plan + build work alone, with the look-back reduced to one poll
+// (mode 4), already takes 5.65 ms -- as long as both passes together.
+constexpr uint32_t kLbSlotU32 = 264; // one block image: lead (<= 23 B) + block (<= 1025 B) + read slack, 16-B multiple
+constexpr uint32_t kLbK = 8;         // blocks per wave (tile = 4 x kLbK blocks)
+constexpr uint32_t kLbArena = 4096;  // bytes of block images per wave
+constexpr uint64_t kLbAgg = 1ull << 63, kLbIncl = 1ull << 62, kLbVal = kLbIncl - 1u;
+constexpr uint64_t kLbWaitTicks = 2000000; // 20 ms of the 100 MHz real-time clock
+static_assert(kPlanHistU32 <= kEncValU32, "plan histogram shares the staging words");
+
+typedef __attribute__((address_space(1))) uint64_t lb_gu64;
+typedef __attribute__((address_space(1))) uint32_t lb_gu32;
+
+__device__ __forceinline__ uint64_t lb_ld(const uint64_t * p)
+{
+    return __hip_atomic_load((lb_gu64 *)(const_cast<uint64_t *>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_st(uint64_t * p, uint64_t v)
+{
+    __hip_atomic_store((lb_gu64 *)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t x) { return readlane_u64(wave_incl_scan64(x), 63); }
+
+// Wave 0 of tile `tile` (> 0): exclusive byte prefix of the tile, or ~0 on
+// abort.  Lane t examines the status words at distances 4t..4t+3 below pos.
+__device__ __forceinline__ uint64_t lb_lookback(const uint64_t * status, uint64_t tile, uint32_t * abort, uint32_t t)
+{
+    uint64_t excl = 0;
+    int64_t pos = static_cast<int64_t>(tile) - 1;
+    const uint64_t t0 = wall_clock64();
+    for (;;)
+    {
+        uint64_t w[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+        {
+            const int64_t idx = pos - static_cast<int64_t>(4u * t + k);
+            w[k] = idx >= 0 ? lb_ld(status + idx) : kLbIncl; // before tile 0: inclusive prefix 0
+        }
+        uint32_t dinc = 0xFFFFu, dinv = 0xFFFFu; // nearest inclusive / unpublished word
+#pragma unroll
+        for (int k = 3; k >= 0; --k)
+        {
+            const uint32_t d = 4u * t + static_cast<uint32_t>(k);
+            dinc = (w[k] & kLbIncl) ? d : dinc;
+            dinv = w[k] == 0u ? d : dinv;
+        }
+        dinc = uni(wave_min(dinc));
+        dinv = uni(wave_min(dinv));
+        if (dinv < dinc)
+        {
+            // a tile before the nearest inclusive prefix has not published yet
+            if (__hip_atomic_load((lb_gu32 *)abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
+                return ~0ull;
+            if (wall_clock64() - t0 > kLbWaitTicks)
+            {
+                if (t == 0)
+                    __hip_atomic_store((lb_gu32 *)abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return ~0ull;
+            }
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        uint64_t s = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            s += (4u * t + k <= dinc) ? (w[k] & kLbVal) : 0u;
+        excl += wave_sum64(s);
+        if (dinc != 0xFFFFu)
+            return excl;
+        pos -= 256;
+    }
+}
+
+// ARENA (bytes per wave, 0 = one fixed 1056-B slot per block): the wave's
+// block images are packed one after the other (16-B aligned) into an arena
+// sized for typical blocks, so more workgroups fit a CU; a block that no
+// longer fits is deferred: after the look-back it is loaded again and built
+// in the (then free) arena one block at a time.
+template <bool D1, uint32_t K, uint32_t ARENA>
+__global__ __launch_bounds__(256) void k_enc256v32_lb(const uint32_t * __restrict in, uint64_t nblocks, const uint32_t * __restrict starts,
+                                                       uint32_t start0, uint64_t * __restrict off, uint8_t * __restrict out, uint64_t out_cap,
+                                                       uint64_t * status, uint32_t * abort)
+{
+    constexpr uint32_t kArenaU32 = ARENA ? ARENA / 4u : K * kLbSlotU32;
+    static_assert(ARENA == 0 || ARENA >= 4u * kLbSlotU32, "the arena must hold one worst-case block");
+    __shared__ __attribute__((aligned(16))) uint32_t arena_all[4][kArenaU32 + 4u]; // + read slack of copy_out_image16
+    __shared__ __attribute__((aligned(16))) uint32_t scr_all[4][kEncValU32];      // plan histogram, then the staged values
+    __shared__ uint64_t xch[5];
+    const uint32_t t = threadIdx.x & 63u;
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    const uint64_t tile = blockIdx.x;
+    uint32_t * const scr = scr_all[wv];
+    uint32_t * const arena = arena_all[wv];
+    EncRun R;
+    R.init_at(in, nblocks, (tile * 4u + wv) * K, K);
+    // lane j: size, image start, image slot (u32x4 index) and plan word of block first+j
+    uint32_t szv = 0u, sbv = 0u, atv = 0u, pwv = 0u;
+    uint32_t built = R.n; // blocks [0, built) are in the arena, the rest deferred
+    const uint32_t stv = (D1 && R.n) ? R.start_lane(in, starts, start0, t) : 0u;
+    if (R.n)
+    {
+        uint32_t pos = 0u; // next free u32x4 of the arena
+        R.walk(t, [&](u32x4 v, uint32_t jj) {
+            if constexpr (D1)
+                v = delta_encode(v, rl32(stv, jj), t);
+            const Plan32 P = plan_block256(v, scr, t);
+            const uint32_t at = ARENA ? pos : jj * (kLbSlotU32 / 4u);
+            const bool fits = ARENA == 0u || (built == R.n && 16u * at + kImgLead + 3u + P.size <= ARENA);
+            wave_lds_sync();
+            uint32_t sb = 0u;
+            if (fits)
+            {
+                uint32_t * img = arena + 4u * at;
+                zero_image(img, min((kImgLead + 3u + P.size + 15u) >> 4, kLbSlotU32 / 4u), t);
+                wave_lds_sync();
+                sb = emit_block256<true>(img, scr, P, v, t);
+                wave_lds_sync();
+                pos = at + ((sb + P.size + 15u) >> 4);
+            }
+            else if (built == R.n)
+                built = jj;
+            szv = t == jj ? P.size : szv;
+            sbv = t == jj ? sb : sbv;
+            atv = t == jj ? at : atv;
+            pwv = t == jj ? plan_word(P) : pwv;
+        });
+    }
+    const uint32_t wt = wave_sum(szv);
+    if (t == 0)
+        xch[wv] = wt;
+    __syncthreads();
+    if (wv == 0)
+    {
+        const uint64_t T = xch[0] + xch[1] + xch[2] + xch[3];
+        uint64_t E = 0;
+        if (tile == 0)
+        {
+            if (t == 0)
+                lb_st(status, kLbIncl | T);
+        }
+        else
+        {
+            if (t == 0)
+                lb_st(status + tile, kLbAgg | T);
+            E = lb_lookback(status, tile, abort, t);
+            if (E != ~0ull && t == 0)
+                lb_st(status + tile, kLbIncl | (E + T));
+        }
+        if (t == 0)
+        {
+            xch[4] = E;
+            if (tile + 1u == gridDim.x && E != ~0ull)
+                off[nblocks] = E + T;
+        }
+    }
+    __syncthreads();
+    const uint64_t E = xch[4];
+    if (E == ~0ull || R.n == 0)
+        return;
+    uint64_t base = E;
+    for (uint32_t w = 0; w < wv; ++w)
+        base += xch[w];
+    const uint32_t incl = wave_incl_scan(szv);
+    const uint64_t ov = base + (incl - szv);
+    if (t < R.n)
+        off[R.first + t] = ov;
+    const uint64_t out_base = reinterpret_cast<uint64_t>(out);
+    for (uint32_t j = 0; j < built; ++j)
+        copy_out_image16(arena + 4u * rl32(atv, j), rl32(sbv, j), out_base + readlane_u64(ov, j), rl32(szv, j), out_base + out_cap, t);
+    for (uint32_t j = built; j < R.n; ++j)
+    {
+        // deferred block: load it again and build it in the arena
+        u32x4 v = R.load(j, t);
+        if constexpr (D1)
+            v = delta_encode(v, rl32(stv, j), t);
+        const uint32_t size = rl32(szv, j);
+        const Plan32 P = unplan(rl32(pwv, j), size);
+        wave_lds_sync();
+        zero_image(arena, (kImgLead + 3u + size + 15u) >> 4, t);
+        wave_lds_sync();
+        const uint32_t sb = emit_block256<true>(arena, scr, P, v, t);
+        wave_lds_sync();
+        copy_out_image16(arena, sb, out_base + readlane_u64(ov, j), size, out_base + out_cap, t);
+    }
 }
 
 // ---- single-launch pipelined encoder: MEASURED AND REJECTED ---
@@ -669,11 +903,101 @@ hipError_t launch_pipe_w(int minw, const uint32_t * in, uint64_t nblocks, const 
     }
 }
 
+// look-back encoder: one status word per tile + the abort word, then the
+// two-pass encoder's workspace for its gated fallback
+uint64_t lb_tiles(uint64_t nblocks, uint32_t k) { return (nblocks + 4u * k - 1u) / (4u * k); }
+size_t lb_status_bytes(uint64_t nblocks) { return al256(lb_tiles(nblocks, 4) * 8u + 16u); } // the smallest tile measured
+
+// look-back encoder variants: {K, ARENA}
+struct LbCfg
+{
+    uint32_t k, arena;
+};
+
+template <bool D1, uint32_t K, uint32_t A>
+void launch_lb_one(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, uint8_t * out, uint64_t out_cap,
+                   uint64_t * off, uint64_t * status, uint32_t * abort, hipStream_t stream)
+{
+    hipLaunchKernelGGL((dev::k_enc256v32_lb<D1, K, A>), dim3(static_cast<uint32_t>(lb_tiles(nblocks, K))), dim3(256), 0, stream, in, nblocks,
+                       starts, start0, off, out, out_cap, status, abort);
+}
+
+template <bool D1>
+hipError_t launch_lb_k(LbCfg c, const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, uint8_t * out,
+                       uint64_t out_cap, uint64_t * off, uint64_t * status, uint32_t * abort, hipStream_t stream)
+{
+#define TPF_LB(K, A)                                                                                        \
+    if (c.k == K && c.arena == A)                                                                           \
+    {                                                                                                       \
+        launch_lb_one<D1, K, A>(in, nblocks, starts, start0, out, out_cap, off, status, abort, stream);      \
+        return hipGetLastError();                                                                           \
+    }
+    TPF_LB(4, 0)
+    TPF_LB(6, 0)
+    TPF_LB(8, 0)
+    TPF_LB(8, 5120)
+    TPF_LB(8, 4096)
+    TPF_LB(6, 3840)
+    TPF_LB(12, 7680)
+#undef TPF_LB
+    return hipErrorInvalidValue;
+}
+
+// plan -> run scan -> write; gate != nullptr: the look-back encoder's fallback
+// (runs only if *gate != 0), launched on a small grid-stride grid
+hipError_t launch_twopass(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, bool d1, uint8_t * out,
+                          uint64_t out_cap, uint64_t * off, void * ws, hipStream_t stream, int probe, const uint32_t * gate)
+{
+    uint32_t * plan = static_cast<uint32_t *>(ws);
+    const uint64_t nruns = enc_runs(nblocks);
+    const RunScanWs<uint64_t> rs = RunScanWs<uint64_t>::carve(static_cast<uint8_t *>(ws) + al256(nblocks * 4u), nruns);
+    const uint64_t per_wg = 4ull * dev::kEncRun;
+    const uint64_t full = (nblocks + per_wg - 1) / per_wg;
+    const uint32_t grid = static_cast<uint32_t>(gate ? std::min<uint64_t>(full, grid_cap(stream, 8)) : full);
+    if (d1)
+        hipLaunchKernelGGL(dev::k_enc256v32_plan<true>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan, rs.tot,
+                           gate);
+    else if (probe == 1)
+        hipLaunchKernelGGL((dev::k_enc256v32_plan<false, 1>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
+                           rs.tot, gate);
+    else
+        hipLaunchKernelGGL(dev::k_enc256v32_plan<false>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan, rs.tot,
+                           gate);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return e;
+    e = launch_run_scan_u64(rs.tot, nruns, rs.pre, rs.tile, off + nblocks, stream, gate);
+    if (e != hipSuccess)
+        return e;
+    if (d1)
+        hipLaunchKernelGGL(dev::k_enc256v32_write<true>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan, rs.pre,
+                           rs.tile, out, out_cap, gate);
+    else if (probe == 2)
+        hipLaunchKernelGGL((dev::k_enc256v32_write<false, 2>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
+                           rs.pre, rs.tile, out, out_cap, gate);
+    else
+        hipLaunchKernelGGL(dev::k_enc256v32_write<false>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
+                           rs.pre, rs.tile, out, out_cap, gate);
+    return hipGetLastError();
+}
+
 } // namespace
 
 // the pipelined encoder's workspace is largest at the smallest chunk it may run with (64 items)
-size_t enc256v32_workspace(uint64_t nblocks) { return std::max(twopass_workspace(nblocks), pipe_geom(nblocks, 64).bytes); }
+size_t enc256v32_workspace(uint64_t nblocks)
+{
+    return std::max(lb_status_bytes(nblocks) + twopass_workspace(nblocks), pipe_geom(nblocks, 64).bytes);
+}
 
+// probe (measurement / test hooks, reachable only through tpf_probe_enc256v32):
+//   0 / 3 production: the two-pass encoder
+//   1 / 2 its passes with the coding removed
+//   4 the look-back encoder (kLbK, kLbArena) with the abort word raised before
+//     the launch (every tile but the first gives up, the fallback encodes the batch)
+//   12 the look-back encoder (kLbK, kLbArena) + its gated two-pass fallback
+//   5 / 6 / 7 the look-back encoder with 4 / 6 / 8 blocks per wave in fixed slots,
+//   8 / 9 / 10 / 11 with arenas {8 blocks, 5120 B}, {8, 4096}, {6, 3840}, {12, 7680} (+ fallback)
+//   >= 16 the rejected single-launch pipelined encoder
 hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, bool d1,
                             uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t stream,
                             int probe)
@@ -687,45 +1011,33 @@ hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_
         // probe >= 16 (measurement): 16 + ci + 1024 * lag + 65536 * minw + 2^20 * per_ticket
         // (minw: launch bound in waves per SIMD, 8 / 6 / other = none)
         const uint32_t pv = static_cast<uint32_t>(probe - 16);
-        const uint32_t ci = probe >= 16 ? std::min<uint32_t>(dev::kPipeMaxChunkItems, std::max<uint32_t>(64, pv % 1024))
-                                        : dev::kPipeChunkItems;
-        const uint32_t lag = probe >= 16 ? std::max<uint32_t>(1, (pv / 1024) % 64) : dev::kPipeLag;
-        const int minw = probe >= 16 ? static_cast<int>((pv >> 16) & 15u) : dev::kPipeMinWaves;
-        const uint32_t per_ticket = probe >= 16 ? std::max<uint32_t>(1, pv >> 20) : dev::kPipePerTicket;
+        const uint32_t ci = std::min<uint32_t>(dev::kPipeMaxChunkItems, std::max<uint32_t>(64, pv % 1024));
+        const uint32_t lag = std::max<uint32_t>(1, (pv / 1024) % 64);
+        const int minw = static_cast<int>((pv >> 16) & 15u);
+        const uint32_t per_ticket = std::max<uint32_t>(1, pv >> 20);
         return d1 ? launch_pipe_w<true>(minw, in, nblocks, starts, start0, out, out_cap, off, ws, stream, ci, lag, per_ticket)
                   : launch_pipe_w<false>(minw, in, nblocks, starts, start0, out, out_cap, off, ws, stream, ci, lag, per_ticket);
     }
-    // the production two-pass encoder (probe 0 / 3), or its passes with the coding removed (probe 1 / 2)
-    if (ws_bytes < twopass_workspace(nblocks))
+    if (ws_bytes < enc256v32_workspace(nblocks))
         return hipErrorInvalidValue;
-    uint32_t * plan = static_cast<uint32_t *>(ws);
-    const uint64_t nruns = enc_runs(nblocks);
-    const RunScanWs<uint64_t> rs = RunScanWs<uint64_t>::carve(static_cast<uint8_t *>(ws) + al256(nblocks * 4u), nruns);
-    const uint64_t per_wg = 4ull * dev::kEncRun;
-    const uint32_t grid = static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg);
-    if (d1)
-        hipLaunchKernelGGL(dev::k_enc256v32_plan<true>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan, rs.tot);
-    else if (probe == 1)
-        hipLaunchKernelGGL((dev::k_enc256v32_plan<false, 1>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
-                           rs.tot);
-    else
-        hipLaunchKernelGGL(dev::k_enc256v32_plan<false>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan, rs.tot);
-    hipError_t e = hipGetLastError();
+    if (probe <= 3)
+        return launch_twopass(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream, probe, nullptr);
+    static const LbCfg cfgs[] = {{dev::kLbK, dev::kLbArena}, {4, 0}, {6, 0}, {8, 0}, {8, 5120}, {8, 4096}, {6, 3840}, {12, 7680}};
+    const LbCfg c = probe >= 5 && probe <= 11 ? cfgs[probe - 4] : cfgs[0]; // 4, 12: cfgs[0]
+    const uint32_t k = c.k;
+    uint64_t * status = static_cast<uint64_t *>(ws);
+    uint32_t * abort = reinterpret_cast<uint32_t *>(status + lb_tiles(nblocks, k));
+    void * tws = static_cast<uint8_t *>(ws) + lb_status_bytes(nblocks);
+    hipError_t e = hipMemsetAsync(status, 0, lb_tiles(nblocks, k) * 8u + 16u, stream);
+    if (e == hipSuccess && probe == 4)
+        e = hipMemsetAsync(abort, 1, 1, stream);
     if (e != hipSuccess)
         return e;
-    e = launch_run_scan_u64(rs.tot, nruns, rs.pre, rs.tile, off + nblocks, stream);
+    e = d1 ? launch_lb_k<true>(c, in, nblocks, starts, start0, out, out_cap, off, status, abort, stream)
+           : launch_lb_k<false>(c, in, nblocks, starts, start0, out, out_cap, off, status, abort, stream);
     if (e != hipSuccess)
         return e;
-    if (d1)
-        hipLaunchKernelGGL(dev::k_enc256v32_write<true>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan, rs.pre,
-                           rs.tile, out, out_cap);
-    else if (probe == 2)
-        hipLaunchKernelGGL((dev::k_enc256v32_write<false, 2>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
-                           rs.pre, rs.tile, out, out_cap);
-    else
-        hipLaunchKernelGGL(dev::k_enc256v32_write<false>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
-                           rs.pre, rs.tile, out, out_cap);
-    return hipGetLastError();
+    return launch_twopass(in, nblocks, starts, start0, d1, out, out_cap, off, tws, stream, 0, abort);
 }
 
 } // namespace tpf

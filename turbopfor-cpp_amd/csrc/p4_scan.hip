@@ -26,11 +26,18 @@ __device__ __forceinline__ T readlane_t(T x, uint32_t l)
 // Tile k = run totals [k*4096, (k+1)*4096): thread i sums its 16 consecutive
 // entries serially, the 256 thread sums are scanned (wave scans + 4 wave
 // totals in LDS); pre[] = exclusive prefix inside the tile, tile[k] = total.
+__device__ __forceinline__ bool scan_gated_off(const uint32_t * gate)
+{
+    return gate != nullptr && __hip_atomic_load(const_cast<uint32_t *>(gate), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+}
+
 template <class T>
 __global__ __launch_bounds__(256) void k_run_scan_tiles(const uint32_t * __restrict tot, uint64_t nruns, T * __restrict pre,
-                                                         T * __restrict tile)
+                                                         T * __restrict tile, const uint32_t * gate)
 {
     __shared__ T wsum[4];
+    if (scan_gated_off(gate))
+        return;
     const uint32_t t = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kScanTile + 16u * threadIdx.x;
     T v[16];
@@ -61,9 +68,11 @@ __global__ __launch_bounds__(256) void k_run_scan_tiles(const uint32_t * __restr
 // One workgroup: exclusive scan of the tile totals in place, 1024 per step
 // with a running carry; *total = the sum of everything.
 template <class T>
-__global__ __launch_bounds__(1024) void k_run_scan_tops(T * __restrict tile, uint64_t ntiles, T * __restrict total)
+__global__ __launch_bounds__(1024) void k_run_scan_tops(T * __restrict tile, uint64_t ntiles, T * __restrict total, const uint32_t * gate)
 {
     __shared__ T wsum[16];
+    if (scan_gated_off(gate))
+        return;
     const uint32_t t = threadIdx.x & 63u, w = threadIdx.x >> 6;
     T carry = 0;
     for (uint64_t c = 0; c < ntiles; c += 1024u)
@@ -106,23 +115,24 @@ namespace tpf
 namespace
 {
 template <class T>
-hipError_t run_scan(const uint32_t * tot, uint64_t nruns, T * pre, T * tile, T * total, hipStream_t s)
+hipError_t run_scan(const uint32_t * tot, uint64_t nruns, T * pre, T * tile, T * total, hipStream_t s, const uint32_t * gate = nullptr)
 {
     if (nruns == 0)
         return total ? hipMemsetAsync(total, 0, sizeof(T), s) : hipSuccess;
     const uint64_t ntiles = RunScanWs<T>::tiles(nruns);
-    hipLaunchKernelGGL(dev::k_run_scan_tiles<T>, dim3(static_cast<uint32_t>(ntiles)), dim3(256), 0, s, tot, nruns, pre, tile);
+    hipLaunchKernelGGL(dev::k_run_scan_tiles<T>, dim3(static_cast<uint32_t>(ntiles)), dim3(256), 0, s, tot, nruns, pre, tile, gate);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return e;
-    hipLaunchKernelGGL(dev::k_run_scan_tops<T>, dim3(1), dim3(1024), 0, s, tile, ntiles, total);
+    hipLaunchKernelGGL(dev::k_run_scan_tops<T>, dim3(1), dim3(1024), 0, s, tile, ntiles, total, gate);
     return hipGetLastError();
 }
 } // namespace
 
-hipError_t launch_run_scan_u64(const uint32_t * tot, uint64_t nruns, uint64_t * pre, uint64_t * tile, uint64_t * total, hipStream_t s)
+hipError_t launch_run_scan_u64(const uint32_t * tot, uint64_t nruns, uint64_t * pre, uint64_t * tile, uint64_t * total, hipStream_t s,
+                               const uint32_t * gate)
 {
-    return run_scan<uint64_t>(tot, nruns, pre, tile, total, s);
+    return run_scan<uint64_t>(tot, nruns, pre, tile, total, s, gate);
 }
 
 hipError_t launch_run_scan_u32(const uint32_t * tot, uint64_t nruns, uint32_t * pre, uint32_t * tile, uint32_t * total, hipStream_t s)

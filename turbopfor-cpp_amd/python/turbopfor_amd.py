@@ -140,9 +140,11 @@ def probe_hbm(kind, dst, src, nbytes):
 
 
 def probe_enc256v32(mode, values, out):
-    """Measurement only: the 256v32 encoder's passes with the coding removed
-    (mode 1 = plan pass as a wave OR, 2 = write pass copying values); the
-    output is not a valid stream."""
+    """Measurement / test hooks of the 256v32 encoder (tpf_probe_enc256v32):
+    mode 1 = plan pass as a wave OR, 2 = write pass copying values (not a
+    valid stream); 3 = two-pass encoder, 4 = look-back encoder forced onto its
+    fallback, 5/6/7 = look-back encoder with 4/6/8 blocks per wave (valid
+    streams).  Returns the offsets tensor [nblocks+1]."""
     import torch
 
     nb = values.numel() // 256
@@ -152,6 +154,7 @@ def probe_enc256v32(mode, values, out):
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=values.device)
     _check(L.tpf_probe_enc256v32(mode, _ptr(values), nb, _ptr(out), out.numel(), _ptr(offs), _ptr(ws), ws_bytes,
                                  _stream(torch)))
+    return offs
 
 
 def enc256v32(values, d1=False, starts=None, start0=0, out=None):
