@@ -91,9 +91,11 @@ struct EncRun
         return true;
     }
 
+    // AUX: cache policy bits of the value loads (2 = nt, 16 = sc1; A/B knob)
+    template <int AUX = 0>
     __device__ __forceinline__ u32x4 load(uint32_t jj, uint32_t t) const
     {
-        return __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(jj * 1024u + 16u * t), 0, 0);
+        return __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(jj * 1024u + 16u * t), 0, AUX);
     }
 
     // Start value of block first+t for delta-1 (lanes t < n): the given
@@ -110,13 +112,13 @@ struct EncRun
     }
 
     // Pipelined walk: body(v, jj) for jj = 0..n-1 with NC blocks in flight.
-    template <class Body>
+    template <int AUX = 0, class Body>
     __device__ __forceinline__ void walk(uint32_t t, Body && body) const
     {
         u32x4 C[kEncNC];
 #pragma unroll
         for (uint32_t u = 0; u + 1 < kEncNC; ++u)
-            C[u] = load(u, t);
+            C[u] = load<AUX>(u, t);
         bool more = true;
         for (uint32_t j = 0; more; j += kEncNC)
         {
@@ -125,7 +127,7 @@ struct EncRun
             {
                 if (more)
                 {
-                    C[(u + kEncNC - 1) % kEncNC] = load(j + u + kEncNC - 1, t);
+                    C[(u + kEncNC - 1) % kEncNC] = load<AUX>(j + u + kEncNC - 1, t);
                     body(C[u], j + u);
                     more = j + u + 1 < n;
                 }
@@ -133,6 +135,10 @@ struct EncRun
         }
     }
 };
+
+// PROBE of the two-pass kernels: bits 0-1 = probe kind (1 plan as a wave OR,
+// 2 write as a copy), bit 8 = nt value loads, bit 9 = sc1 value loads (A/B)
+constexpr int enc_load_aux(int probe) { return ((probe & 256) ? 2 : 0) | ((probe & 512) ? 16 : 0); }
 
 __device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t lane)
 {
@@ -147,11 +153,11 @@ __device__ __forceinline__ void plan_run(const EncRun & R, const uint32_t * in, 
     const uint32_t stv = D1 ? R.start_lane(in, starts, start0, t) : 0u;
     szv = 0u;
     pwv = 0u;
-    R.walk(t, [&](u32x4 v, uint32_t jj) {
+    R.template walk<enc_load_aux(PROBE)>(t, [&](u32x4 v, uint32_t jj) {
         if constexpr (D1)
             v = delta_encode(v, rl32(stv, jj), t);
         Plan32 P;
-        if constexpr (PROBE == 1)
+        if constexpr ((PROBE & 3) == 1)
         {
             P.b = bw32(uni(wave_or(v.x | v.y | v.z | v.w)));
             P.bx = 0;
@@ -174,13 +180,13 @@ __device__ __forceinline__ void write_run(const EncRun & R, const uint32_t * in,
                                           uint32_t * val, uint64_t out_base, uint64_t cap_end, uint32_t t)
 {
     const uint32_t stv = D1 ? R.start_lane(in, starts, start0, t) : 0u;
-    R.walk(t, [&](u32x4 v, uint32_t jj) {
+    R.template walk<enc_load_aux(PROBE)>(t, [&](u32x4 v, uint32_t jj) {
         if constexpr (D1)
             v = delta_encode(v, rl32(stv, jj), t);
         const uint32_t size = rl32(szv, jj);
         const Plan32 P = unplan(rl32(pwv, jj), size);
         const uint64_t dst = out_base + ((static_cast<uint64_t>(rl32(ohi, jj)) << 32) | rl32(olo, jj));
-        if constexpr (PROBE == 2)
+        if constexpr ((PROBE & 3) == 2)
         {
             reinterpret_cast<u32x4 *>(img)[4 + t] = v;
             wave_lds_sync();
@@ -957,6 +963,12 @@ hipError_t launch_twopass(const uint32_t * in, uint64_t nblocks, const uint32_t 
     if (d1)
         hipLaunchKernelGGL(dev::k_enc256v32_plan<true>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan, rs.tot,
                            gate);
+    else if (probe == 13)
+        hipLaunchKernelGGL((dev::k_enc256v32_plan<false, 256>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
+                           rs.tot, gate);
+    else if (probe == 14)
+        hipLaunchKernelGGL((dev::k_enc256v32_plan<false, 512>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
+                           rs.tot, gate);
     else if (probe == 1)
         hipLaunchKernelGGL((dev::k_enc256v32_plan<false, 1>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
                            rs.tot, gate);
@@ -974,6 +986,12 @@ hipError_t launch_twopass(const uint32_t * in, uint64_t nblocks, const uint32_t 
                            rs.tile, out, out_cap, gate);
     else if (probe == 2)
         hipLaunchKernelGGL((dev::k_enc256v32_write<false, 2>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
+                           rs.pre, rs.tile, out, out_cap, gate);
+    else if (probe == 13 || probe == 15)
+        hipLaunchKernelGGL((dev::k_enc256v32_write<false, 256>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
+                           rs.pre, rs.tile, out, out_cap, gate);
+    else if (probe == 14)
+        hipLaunchKernelGGL((dev::k_enc256v32_write<false, 512>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
                            rs.pre, rs.tile, out, out_cap, gate);
     else
         hipLaunchKernelGGL(dev::k_enc256v32_write<false>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
@@ -995,6 +1013,8 @@ size_t enc256v32_workspace(uint64_t nblocks)
 //   4 the look-back encoder (kLbK, kLbArena) with the abort word raised before
 //     the launch (every tile but the first gives up, the fallback encodes the batch)
 //   12 the look-back encoder (kLbK, kLbArena) + its gated two-pass fallback
+//   13 / 14 the two-pass encoder with nt / sc1 value loads in both passes,
+//   15 with nt value loads in the write pass only
 //   5 / 6 / 7 the look-back encoder with 4 / 6 / 8 blocks per wave in fixed slots,
 //   8 / 9 / 10 / 11 with arenas {8 blocks, 5120 B}, {8, 4096}, {6, 3840}, {12, 7680} (+ fallback)
 //   >= 16 the rejected single-launch pipelined encoder
@@ -1020,7 +1040,7 @@ hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_
     }
     if (ws_bytes < enc256v32_workspace(nblocks))
         return hipErrorInvalidValue;
-    if (probe <= 3)
+    if (probe <= 3 || probe >= 13)
         return launch_twopass(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream, probe, nullptr);
     static const LbCfg cfgs[] = {{dev::kLbK, dev::kLbArena}, {4, 0}, {6, 0}, {8, 0}, {8, 5120}, {8, 4096}, {6, 3840}, {12, 7680}};
     const LbCfg c = probe >= 5 && probe <= 11 ? cfgs[probe - 4] : cfgs[0]; // 4, 12: cfgs[0]
