@@ -348,6 +348,14 @@ extern "C" int decvar_launch(int deal, int probe, const void * in, uint64_t in_b
         case 41: return launch_nc<4, 8, true>(A, s);
         case 42: return launch_nc<5, 8, false>(A, s);
         case 43: return launch_nc<5, 8, true>(A, s);
+        case 44: return launch_nc<8, 5, false>(A, s);
+        case 45: return launch_nc<8, 5, true>(A, s);
+        case 46: return launch_nc<12, 4, false>(A, s);
+        case 47: return launch_nc<12, 4, true>(A, s);
+        case 48: return launch_nc<16, 4, false>(A, s);
+        case 49: return launch_nc<16, 4, true>(A, s);
+        case 50: return launch_nc<8, 4, false>(A, s);
+        case 51: return launch_nc<8, 4, true>(A, s);
         default: return -2;
     }
 }

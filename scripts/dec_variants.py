@@ -27,7 +27,7 @@ V.decvar_launch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.
                             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
 DEALS = {0: "runs", 1: "wg-rr", 2: "global", 3: "xcd", 4: "global32", 5: "xk2", 6: "xk8", 7: "xk32", 8: "xk128",
          9: "xk512", 10: "vb1", 11: "vb2", 12: "vb3", 13: "st-plain", 14: "st-nt", 15: "st-sc1", 16: "st-sc0sc1",
-         17: "st-sc1nt", 18: "st-sc0nt", 19: "st-sc0sc1nt", 20: "nc4w8", 21: "nc5w8"}
+         17: "st-sc1nt", 18: "st-sc0nt", 19: "st-sc0sc1nt", 20: "nc4w8", 21: "nc5w8", 22: "nc8w5", 23: "nc12w4", 24: "nc16w4", 25: "nc8w4"}
 NOPROBE = {10, 11, 12}
 if os.environ.get("DEALS"):
     DEALS = {int(k): v for k, v in DEALS.items() if str(k) in os.environ["DEALS"].split(",")}
