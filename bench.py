@@ -739,7 +739,7 @@ def run_c3(args, world, rank, dev, T, chained):
             "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             **traffic_fields("c3chain" if chained else "c3", nb),
             "kernel_ms_avg": round(avg_ms, 4),
-            "kernel": ("k_dec256v32w<SumOnly> + run scan (2 small kernels) + k_dec256v32w<Prefix>" if chained
+            "kernel": ("k_dsum256v32w (phase A) + run scan (2 small kernels) + k_dec256v32w<Prefix>" if chained
                        else "tpf::dev::k_dec256v32w<StartMode::PerBlock>"),
             "probe_GBps": round(probe_alg / (float(np.mean(probe_ms)) * 1e-3) / 1e9, 1),
             "ms_vs_probe": round(avg_ms / float(np.mean(probe_ms)), 3),

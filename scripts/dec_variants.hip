@@ -295,7 +295,87 @@ int launch_nc(const VArgs & A0, hipStream_t s)
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// ---- chained-D1 phase A (block delta sums) with another pipeline depth /
+// occupancy / run length: sums[i] = the product's phase A block sum ----------
+template <uint32_t NC, int MINW, uint32_t kRun>
+__global__ __launch_bounds__(256, MINW) void k_sum(const VArgs A)
+{
+    __shared__ uint32_t slots[4][kSlotBytes / 4];
+    const uint32_t t = threadIdx.x & 63u;
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    const uint64_t first = (static_cast<uint64_t>(blockIdx.x) * 4u + wv) * kRun;
+    if (first >= A.nblocks)
+        return;
+    uint32_t * slot = slots[wv];
+    const uint64_t in_base = reinterpret_cast<uint64_t>(A.in);
+    const uint32_t n = static_cast<uint32_t>(min_u64(kRun, A.nblocks - first));
+    const bool valid = t < n;
+    const uint64_t o = valid ? A.off[first + t] : 0ull;
+    const uint64_t e = valid ? A.off[first + t + 1u] : 0ull;
+    RunPlaneT<kSlotBytes, true> P;
+    P.init(in_base, in_base + A.in_bytes, o, e, valid);
+    uint32_t sumv = 0u;
+    auto issue = [&](Chunk & c, uint32_t jj) { P.template issue<2>(c, jj, t); };
+    auto consume = [&](const Chunk & c, uint32_t jj) {
+        const uint32_t ctl = P.stage(c, jj, slot, t);
+        uint32_t used;
+        const uint32_t sm = dsum_block256v32(slot, (ctl >> kCtlShift) & 15u, t, used);
+        sumv = t == jj ? sm : sumv;
+        wave_lds_sync();
+    };
+    Chunk C[NC];
+#pragma unroll
+    for (uint32_t u = 0; u + 1 < NC; ++u)
+        issue(C[u], u);
+    bool more = true;
+    for (uint32_t j = 0; more; j += NC)
+    {
+#pragma unroll
+        for (uint32_t u = 0; u < NC; ++u)
+        {
+            if (more)
+            {
+                issue(C[(u + NC - 1) % NC], j + u + NC - 1);
+                consume(C[u], j + u);
+                more = j + u + 1 < n;
+            }
+        }
+    }
+    if (valid)
+        A.out[first + t] = sumv;
+}
+
+template <uint32_t NC, int MINW, uint32_t kRun>
+int launch_sum(const VArgs & A, hipStream_t s)
+{
+    const uint32_t grid = static_cast<uint32_t>((A.nblocks + 4u * kRun - 1u) / (4u * kRun));
+    hipLaunchKernelGGL((k_sum<NC, MINW, kRun>), dim3(grid), dim3(256), 0, s, A);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 } // namespace tpf::dev
+
+// phase A variants: out = u32 block sums
+extern "C" int decvar_sums(int v, const void * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, void * out, void * stream)
+{
+    using namespace tpf::dev;
+    const VArgs A{static_cast<const uint8_t *>(in), in_bytes, off, nblocks, static_cast<uint32_t *>(out), 0u, nullptr};
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    if (nblocks == 0)
+        return 0;
+    switch (v)
+    {
+        case 0: return launch_sum<6, 7, 16>(A, s); // the product's configuration
+        case 1: return launch_sum<4, 8, 16>(A, s);
+        case 2: return launch_sum<3, 8, 16>(A, s);
+        case 3: return launch_sum<8, 6, 16>(A, s);
+        case 4: return launch_sum<6, 7, 32>(A, s);
+        case 5: return launch_sum<4, 8, 32>(A, s);
+        case 6: return launch_sum<2, 8, 16>(A, s);
+        case 7: return launch_sum<12, 4, 16>(A, s);
+        default: return -2;
+    }
+}
 
 extern "C" int decvar_launch(int deal, int probe, const void * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, void * out,
                              unsigned long long * err, void * stream)

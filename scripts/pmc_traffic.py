@@ -29,7 +29,7 @@ KERNELS = {
     "c1": ([lambda n: "k_dec_gr" in n and ("FmtE0E" in n or "Fmt)0," in n)], "tpf::dev::k_dec_gr<Fmt::H32>"),
     # chained list: phase A (block sums) + phase B (prefix decode); the run
     # scan between them (p4_scan.hip: 625K u32 run sums, ~5 MB) is not counted
-    "c3chain": ([_dec(3), _dec(2)], "k_dec256v32w<SumOnly> + k_dec256v32w<Prefix>"),
+    "c3chain": ([lambda n: "k_dsum256v32w" in n, _dec(2)], "k_dsum256v32w (phase A) + k_dec256v32w<Prefix>"),
     # round trip: encoder plan + write passes (non-D1) + decode; the run
     # scan between the passes (625K run totals, ~7.5 MB) is not counted
     "c4": ([lambda n: "k_enc256v32_plan" in n and ("ILb0E" in n or "<false" in n),

@@ -20,7 +20,8 @@ def _list(nb, start0, seed):
     return vals, starts
 
 
-@pytest.mark.parametrize("start0,nb", [(0, 5000), (7, 5000), (0xFFFFFF00, 5000), (5, 1), (5, 3), (5, 4), (5, 5),
+@pytest.mark.parametrize("start0,nb", [(0, 5000), (7, 5000), (0xFFFFFF00, 5000), (5, 1), (5, 3), (5, 4), (5, 5), (9, 16), (9, 17), (9, 31),
+                                      (9, 32), (9, 33), (9, 48), (9, 65), (9, 130), (9, 4111),
                                        (5, 257), (11, 200003)])
 def test_chained_single(start0, nb):
     vals, starts = _list(nb, start0, seed=3)

@@ -15,12 +15,16 @@
 namespace tpf::dev
 {
 
+// blocks per run of the chained decode's phase A (k_dsum256v32w): one run sum
+// each for the run scan; phase B's 16-block runs nest in them
+constexpr uint32_t kSumRun = 32;
+
 enum class StartMode : int
 {
     None = 0,     // p4Dec256v32
     PerBlock = 1, // p4D1Dec256v32, start of block i = starts[i]
     Prefix = 2,   // chained list: start of block i = base + sum of the block sums before i (run scan, p4_scan.h)
-    SumOnly = 3,  // no output: sums[i] = sum over the block of (v + 1) mod 2^32
+    // 3 was SumOnly (phase A of the chained decode): now k_dsum256v32w
     Probe = 4,    // measurement only: same loads and stores, no decode (data-movement ceiling)
 };
 
@@ -33,9 +37,9 @@ struct DecArgs
     uint32_t * out;
     const uint32_t * starts; // PerBlock: starts; Prefix: the block sums of phase A
     uint32_t base;           // Prefix: value preceding block 0
-    uint32_t * sums;         // SumOnly: block sums
+    uint32_t * sums;         // k_dsum256v32w: block sums
     unsigned long long * err;
-    uint32_t * run_tot = nullptr;        // SumOnly: one sum per wave run
+    uint32_t * run_tot = nullptr;        // k_dsum256v32w: one sum per wave run
     const uint32_t * run_pre = nullptr;  // Prefix: run scan (p4_scan.h)
     const uint32_t * run_tile = nullptr; // Prefix: run scan (p4_scan.h)
 };
@@ -86,12 +90,18 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
         startv = valid ? A.starts[blk] : 0u;
     if constexpr (SM == StartMode::Prefix)
     {
-        // base + the run's base + the sums of the run's earlier blocks (mod 2^32)
-        const uint32_t sv = valid ? A.starts[blk] : 0u;
-        startv = A.base + run_base(A.run_pre, A.run_tile, first / kRun) + (wave_incl_scan(sv) - sv);
+        // base + the base of phase A's kSumRun-block run holding this one +
+        // the sums of that run's blocks before each block (mod 2^32): lanes
+        // 0..kSumRun-1 scan the run's block sums, lane t takes entry k + t
+        static_assert(kSumRun % kRun == 0 && kSumRun <= 64 && (POL & 4u) == 0u, "prefix runs nest in phase A's runs");
+        const uint64_t f = first / kSumRun * kSumRun;
+        const uint32_t k = static_cast<uint32_t>(first - f);
+        const uint32_t sv = (t < kSumRun && f + t < A.nblocks) ? A.starts[f + t] : 0u;
+        const uint32_t ex = wave_incl_scan(sv) - sv;
+        startv = A.base + run_base(A.run_pre, A.run_tile, first / kSumRun)
+                 + static_cast<uint32_t>(__shfl(static_cast<int>(ex), static_cast<int>((k + t) & 63u), 64));
     }
-    uint32_t sumv = 0u;
-    uint32_t * const out_run = SM == StartMode::SumOnly ? nullptr : A.out + first * 256u;
+    uint32_t * const out_run = A.out + first * 256u;
     // POL bit 3: the run's output through one buffer descriptor, stored
     // "sc1 nt" (streamed and not kept in the XCD's L2): 1-2.5% over nt alone
     // on every stream shape (scripts/dec_variants.hip)
@@ -102,8 +112,7 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
         else
             st16<POL>(reinterpret_cast<u32x4 *>(out_run + jj * stride * 256u) + t, v);
     };
-    uint64_t badmask = 0u;
-    constexpr bool sum_pass = SM == StartMode::SumOnly;
+    UsedLanes usedv;
 
     auto issue = [&](Chunk & c, uint32_t jj) { P.template issue<POL>(c, jj, t); };
     auto consume = [&](const Chunk & c, uint32_t jj) {
@@ -114,22 +123,12 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
         }
         const uint32_t ctl = P.stage(c, jj, slot, t);
         u32x4 v;
-        uint32_t used;
-        if constexpr (sum_pass)
-        {
-            const uint32_t s = dsum_block256v32(slot, (ctl >> kCtlShift) & 15u, t, used);
-            sumv = t == jj ? s : sumv;
-        }
-        else
-        {
-            used = decode_block256v32(slot, (ctl >> kCtlShift) & 15u, P.head(c, ctl, slot), scr, t, v);
-            if constexpr (SM == StartMode::PerBlock || SM == StartMode::Prefix)
-                apply_delta1_256(v, rl(startv, jj));
-            put(jj, v);
-        }
+        const uint32_t used = decode_block256v32(slot, (ctl >> kCtlShift) & 15u, P.head(c, ctl, slot), scr, t, v);
+        if constexpr (SM == StartMode::PerBlock || SM == StartMode::Prefix)
+            apply_delta1_256(v, rl(startv, jj));
+        put(jj, v);
         wave_lds_sync();
-        if (used != rl(P.len, jj))
-            badmask |= 1ull << jj;
+        usedv.put(used, jj, t);
     };
 
     // NC register chunks rotate (loop unrolled by NC, no copies): while block
@@ -155,14 +154,67 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
         }
     };
     run_pass();
-    if constexpr (SM == StartMode::SumOnly)
-    {
-        if (valid)
-            A.sums[blk] = sumv;
-        publish_run_total(A.run_tot, first / kRun, valid ? sumv : 0u, t);
-    }
+    const uint64_t badmask = usedv.bad(P.len, valid);
     if (A.err != nullptr && t == 0 && badmask != 0u)
         atomicMin(A.err, static_cast<unsigned long long>(first + stride * __builtin_ctzll(badmask)));
+}
+
+// Phase A of the chained decode as its own kernel: block delta sums
+// (dsum_block256v32, no output, no decode scratch), one sum per kSumRun-block
+// run for the run scan.  Runs of 32 with 4 blocks in flight at 8 waves/SIMD:
+// -4% against 16-block runs with 6 in flight at 7 (scripts/chain_sum_variants.py,
+// same-box A/B of the phase on 10M C3 blocks).
+template <uint32_t NC, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_dsum256v32w(const DecArgs A)
+{
+    __shared__ uint32_t slots[4][kSlotBytes / 4];
+    const uint32_t t = threadIdx.x & 63u;
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    const uint64_t first = (static_cast<uint64_t>(blockIdx.x) * 4u + wv) * kSumRun;
+    if (first >= A.nblocks)
+        return;
+    uint32_t * slot = slots[wv];
+    const uint64_t in_base = reinterpret_cast<uint64_t>(A.in);
+    const uint32_t n = static_cast<uint32_t>(min_u64(kSumRun, A.nblocks - first));
+    const bool valid = t < n;
+    const uint64_t o = valid ? A.off[first + t] : 0ull;
+    const uint64_t e = valid ? A.off[first + t + 1u] : 0ull;
+    RunPlaneT<kSlotBytes, true> P;
+    P.init(in_base, in_base + A.in_bytes, o, e, valid);
+    uint32_t sumv = 0u;
+    UsedLanes usedv;
+    auto consume = [&](const Chunk & c, uint32_t jj) {
+        const uint32_t ctl = P.stage(c, jj, slot, t);
+        uint32_t used;
+        const uint32_t sm = dsum_block256v32(slot, (ctl >> kCtlShift) & 15u, t, used);
+        sumv = t == jj ? sm : sumv;
+        wave_lds_sync();
+        usedv.put(used, jj, t);
+    };
+    Chunk C[NC];
+#pragma unroll
+    for (uint32_t u = 0; u + 1 < NC; ++u)
+        P.template issue<2>(C[u], u, t);
+    bool more = true;
+    for (uint32_t j = 0; more; j += NC)
+    {
+#pragma unroll
+        for (uint32_t u = 0; u < NC; ++u)
+        {
+            if (more)
+            {
+                P.template issue<2>(C[(u + NC - 1) % NC], j + u + NC - 1, t);
+                consume(C[u], j + u);
+                more = j + u + 1 < n;
+            }
+        }
+    }
+    if (valid)
+        A.sums[first + t] = sumv;
+    publish_run_total(A.run_tot, first / kSumRun, valid ? sumv : 0u, t);
+    const uint64_t badmask = usedv.bad(P.len, valid);
+    if (A.err != nullptr && t == 0 && badmask != 0u)
+        atomicMin(A.err, static_cast<unsigned long long>(first + __builtin_ctzll(badmask)));
 }
 
 } // namespace tpf::dev
@@ -214,6 +266,8 @@ hipError_t launch_dec256v32(const uint8_t * in, uint64_t in_bytes, const uint64_
 // Workspace: block sums (u32) + the run scan.
 namespace
 {
+// workspace carve count (both phases carve the same layout; phase A scans
+// only its nblocks / kSumRun run sums)
 uint64_t chain_runs(uint64_t nblocks) { return (nblocks + dev::kRunDefault - 1u) / dev::kRunDefault; }
 size_t al256(size_t x) { return (x + 255u) & ~size_t(255); }
 } // namespace
@@ -231,10 +285,12 @@ hipError_t launch_d1chain_sums(const uint8_t * in, uint64_t in_bytes, const uint
     const RunScanWs<uint32_t> rs = RunScanWs<uint32_t>::carve(static_cast<uint8_t *>(ws) + al256(nblocks * 4u), chain_runs(nblocks));
     dev::DecArgs A{in, in_bytes, off, nblocks, nullptr, nullptr, 0u, sums, err};
     A.run_tot = rs.tot;
-    hipError_t e = launch_mode<dev::StartMode::SumOnly>(A, stream);
+    constexpr uint64_t per_wg = 4ull * dev::kSumRun;
+    hipLaunchKernelGGL((dev::k_dsum256v32w<4, 8>), dim3(static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg)), dim3(256), 0, stream, A);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return e;
-    return launch_run_scan_u32(rs.tot, chain_runs(nblocks), rs.pre, rs.tile, total, stream);
+    return launch_run_scan_u32(rs.tot, (nblocks + dev::kSumRun - 1u) / dev::kSumRun, rs.pre, rs.tile, total, stream);
 }
 
 hipError_t launch_d1chain_decode(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * out,

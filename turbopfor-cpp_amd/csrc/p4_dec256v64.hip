@@ -145,7 +145,7 @@ __global__ __launch_bounds__(256, 4) void k_dec128v64w(const uint8_t * __restric
     RunPlaneT<kSlot64> P;
     P.init(in_base, in_base + in_bytes, o, e, valid);
     const uint64_t startv = (D1 && valid) ? starts[unit] : 0ull;
-    uint64_t badmask = 0u;
+    UsedLanes usedv;
     uint64_t * const out_run = out + first * (128u * NB);
 
     auto consume = [&](const Chunk & c, uint32_t jj) {
@@ -164,8 +164,7 @@ __global__ __launch_bounds__(256, 4) void k_dec128v64w(const uint8_t * __restric
             __builtin_nontemporal_store(u64x2{x0, x1}, reinterpret_cast<u64x2 *>(out_run + (jj * NB + u) * 128u) + t);
             wave_lds_sync();
         }
-        if (s - s0 != rl(P.len, jj))
-            badmask |= 1ull << jj;
+        usedv.put(s - s0, jj, t);
     };
 
     Chunk C[NC];
@@ -186,6 +185,7 @@ __global__ __launch_bounds__(256, 4) void k_dec128v64w(const uint8_t * __restric
             }
         }
     }
+    const uint64_t badmask = usedv.bad(P.len, valid);
     if (err != nullptr && t == 0 && badmask != 0u)
         atomicMin(err, static_cast<unsigned long long>(first + __builtin_ctzll(badmask)));
 }

@@ -62,6 +62,19 @@ __device__ __forceinline__ void st16(u32x4 * p, const u32x4 & v)
 // ONE: one 16-byte load per lane per block in flight (the block's first
 // 1 KB; the rest of a larger block is loaded when it is staged), so twice as
 // many blocks fit in flight in the same registers.
+// Length check of a run without per-block scalar work: lane jj keeps the
+// byte count block jj consumed (one v_cndmask per block); after the run one
+// compare against the plane's expected lengths and a ballot give the blocks
+// whose parse disagrees with their offsets.  (The per-block form -- readlane,
+// scalar compare, 64-bit mask update -- put ~5 more SALU instructions on
+// every block.)
+struct UsedLanes
+{
+    uint32_t v = 0u;
+    __device__ __forceinline__ void put(uint32_t used, uint32_t jj, uint32_t t) { v = t == jj ? used : v; }
+    __device__ __forceinline__ uint64_t bad(uint32_t len, bool valid) const { return __ballot(valid && v != len); }
+};
+
 template <uint32_t SLOT, bool ONE = false>
 struct RunPlaneT
 {

@@ -90,6 +90,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void k_de
             if (t + 64u * j < lim)
                 __builtin_nontemporal_store(v[j], op + t + 64u * j);
         wave_lds_sync();
+        // per-block scalar check kept here: the lane-held form (UsedLanes,
+        // p4_dec_run.h) measured -2.3% on C1 (A/B on one box)
         if (used != rl(P.len, jj))
             badmask |= 1ull << jj;
     };
