@@ -531,10 +531,8 @@ __global__ __launch_bounds__(256) void k_enc256v32_lb(const uint32_t * __restric
 constexpr uint32_t kPipeRun = 32;
 constexpr uint32_t kPipeItem = 4u * kPipeRun;
 constexpr uint32_t kPipeMaxChunkItems = 512; // the last arriver's scan covers 2 items per thread
-constexpr uint32_t kPipeChunkItems = 256;    // default: 32K blocks = 32 MiB of values per chunk
-constexpr uint32_t kPipeLag = 2;             // default: chunk c is written in step c + 2
-constexpr int kPipeMinWaves = 8;             // default launch bound: 8 waves per SIMD
-constexpr uint32_t kPipePerTicket = 8;       // default: sequence entries per ticket
+// (the measured configurations -- chunk items, lag, launch bound, entries
+// per ticket -- are all taken from the probe mode)
 constexpr uint32_t kSpinLimit = 1u << 22;    // polls of ~0.2 us
 
 typedef __attribute__((address_space(1))) uint32_t gu32;
