@@ -4,13 +4,13 @@ bench.py reports as roofline.traffic.  Per MI355X_MICROARCH.md §HBM:
 FETCH_SIZE counts half the bytes of 16 B/lane streaming reads on gfx950
 (double it), WRITE_SIZE is exact for 16 B/lane stores; both are in KiB.
 
-Each entry records the md5 of the library the counters were taken with
-(lib_md5) and a label: bench.py replays the number only while it runs that
-same library, and says so (roofline.traffic_source).
+Each entry records the md5 of the library sources the counters were taken
+with (src_md5, turbopfor_amd.source_md5) and a label: bench.py replays the
+number only while it runs code built from those same sources, and says so
+(roofline.traffic_source).
 
 usage: python scripts/pmc_traffic.py WORKLOAD FETCH_CSV WRITE_CSV NBLOCKS OUT_JSON [LABEL]"""
 import csv
-import hashlib
 import json
 import os
 import statistics
@@ -47,14 +47,8 @@ def per_launch(path, counter, test):
 
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "turbopfor-cpp_amd", "lib", "libturbopfor_amd.so")
-
-
-def lib_md5(path=LIB):
-    try:
-        return hashlib.md5(open(path, "rb").read()).hexdigest()
-    except OSError:
-        return None
+sys.path.insert(0, os.path.join(ROOT, "turbopfor-cpp_amd", "python"))
+import turbopfor_amd  # noqa: E402  (source_md5 only: no GPU, no torch import)
 
 
 def main():
@@ -72,7 +66,7 @@ def main():
     hbm = (2.0 * f_kib + w_kib) * 1024.0
     d = {"workload": wl, "nblocks": nblocks, "kernel": kname,
          "FETCH_SIZE_KiB_median": f_kib, "WRITE_SIZE_KiB_median": w_kib, "launches": [nf, nw],
-         "hbm_bytes_per_launch": int(hbm), "label": label, "lib_md5": lib_md5(),
+         "hbm_bytes_per_launch": int(hbm), "label": label, "src_md5": turbopfor_amd.source_md5(),
          "correction": "hbm = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (gfx950 FETCH_SIZE halves 16B/lane reads)"}
     allv = {}
     if os.path.exists(out):
