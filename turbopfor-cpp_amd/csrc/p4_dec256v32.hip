@@ -112,7 +112,10 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
         else
             st16<POL>(reinterpret_cast<u32x4 *>(out_run + jj * stride * 256u) + t, v);
     };
-    UsedLanes usedv;
+    // per-block scalar length check: the lane-held form (UsedLanes) costs one
+    // more VGPR, which at 7 waves/SIMD made the PerBlock/Prefix modes spill
+    // (12 B/lane of scratch: C3 WRITE_SIZE +3%)
+    uint64_t badmask = 0u;
 
     auto issue = [&](Chunk & c, uint32_t jj) { P.template issue<POL>(c, jj, t); };
     auto consume = [&](const Chunk & c, uint32_t jj) {
@@ -128,7 +131,8 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
             apply_delta1_256(v, rl(startv, jj));
         put(jj, v);
         wave_lds_sync();
-        usedv.put(used, jj, t);
+        if (used != rl(P.len, jj))
+            badmask |= 1ull << jj;
     };
 
     // NC register chunks rotate (loop unrolled by NC, no copies): while block
@@ -154,7 +158,6 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
         }
     };
     run_pass();
-    const uint64_t badmask = usedv.bad(P.len, valid);
     if (A.err != nullptr && t == 0 && badmask != 0u)
         atomicMin(A.err, static_cast<unsigned long long>(first + stride * __builtin_ctzll(badmask)));
 }
