@@ -24,7 +24,7 @@ V.decvar_sums.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes
                           ctypes.c_void_p]
 L = tpf.lib()
 NAMES = {0: "nc6w7r16", 1: "nc4w8r16", 2: "nc3w8r16", 3: "nc8w6r16", 4: "nc6w7r32", 5: "nc4w8r32", 6: "nc2w8r16",
-         7: "nc12w4r16"}
+         7: "nc12w4r16", 8: "defer_nc4w8r32", 9: "defer_nc4w8r16", 10: "defer_nc6w7r16"}
 vals, starts = bench.gen_c3(nb, seed=7, dev=dev)
 packed, offs = tpf.enc256v32(vals.view(-1), d1=True, starts=starts)
 del vals, starts

@@ -295,6 +295,161 @@ int launch_nc(const VArgs & A0, hipStream_t s)
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// dsum_block256v32 (p4_block32.h) returning the lane's partial sum: the
+// block sums are then reduced once per run (LDS transpose) instead of one
+// wave reduction per block -- measurement of that reduction's cost
+__device__ __forceinline__ uint32_t dsum_partial256v32(const uint32_t * lds, uint32_t s, uint32_t t, uint32_t & used)
+{
+    const uint32_t hw = uni(lds_u32(lds, s));
+    const uint32_t h = hw & 0xFFu, x1 = (hw >> 8) & 0xFFu;
+    if ((h & 0xC0u) == 0xC0u)
+    {
+        const uint32_t b = h & 0x3Fu;
+        uint32_t c = uni(lds_u32(lds, s + 1u));
+        if (b < 32u)
+            c &= mask32(b);
+        used = 1u + ((b + 7u) >> 3);
+        return t == 0 ? 256u * (c + 1u) : 0u;
+    }
+    uint32_t exsum = 0u, b, p;
+    if ((h & 0x40u) == 0u)
+    {
+        const uint32_t hdr = (h & 0x80u) ? 2u : 1u;
+        const uint32_t bx = (h & 0x80u) ? min(x1, 32u) : 0u;
+        b = min(h & 0x7Fu, 32u);
+        p = s + hdr;
+        if (bx != 0u)
+        {
+            // xn = popcount of the 256-bit bitmap (lane t reads word t & 7)
+            const uint32_t pc = __builtin_popcount(lds_u32(lds, s + 2u + 4u * (t & 7u)));
+            const uint32_t xn = wave_sum((t < 8u) ? pc : 0u);
+            const uint32_t xs = s + 34u;
+            // uniform trip count, predicated adds: a divergent per-lane loop
+            // costs exec-mask (SALU) work every block, and this pass is bound
+            // by its scalar issue (SQ_INSTS_SALU); lanes past xn
+            // read in-slot bytes and add nothing
+            for (uint32_t k0 = 0; k0 < xn; k0 += kWave)
+            {
+                const uint32_t x = lds_bits(lds, xs * 8u + (k0 + t) * bx, bx);
+                exsum += k0 + t < xn ? x : 0u;
+            }
+            p = xs + ((xn * bx + 7u) >> 3);
+        }
+        used = p + 32u * b - s;
+    }
+    else
+    {
+        b = min(h & 0x3Fu, 32u);
+        const uint32_t xn = x1;
+        p = s + 2u;
+        const uint32_t v0 = p + 32u * b;
+        const uint32_t first = uni(lds_byte(lds, v0));
+        uint32_t vend;
+        if (first == 0xFFu)
+        {
+            for (uint32_t k0 = 0; k0 < xn; k0 += kWave)
+            {
+                const uint32_t x = lds_u32(lds, v0 + 1u + 4u * (k0 + t));
+                exsum += k0 + t < xn ? x : 0u;
+            }
+            vend = v0 + 1u + 4u * xn;
+        }
+        else
+        {
+            // the window walk of vbyte_exceptions, summing instead of storing
+            uint32_t c = v0, sp = 0, found = 0;
+            vend = v0;
+            while (found < xn)
+            {
+                const uint32_t by0 = lds_byte(lds, c + t);
+                const uint32_t len0 = by0 < 0x9Cu ? 1u : by0 < 0xDCu ? 2u : by0 < 0xFCu ? 3u : by0 == 0xFCu ? 4u : 5u;
+                const uint32_t q = window_starts(t + len0, sp, t);
+                const uint32_t m = static_cast<uint32_t>(__builtin_popcountll(__ballot(q < 64u)));
+                const uint32_t cnt = min(m, xn - found);
+                const uint32_t qn = bperm(t + len0, q);
+                const uint32_t qe = q < 64u ? qn : q;
+                {
+                    // every lane decodes (q <= 68: in-slot bytes), lanes >= cnt add nothing
+                    const uint32_t by = lds_byte(lds, c + q);
+                    const uint32_t d = lds_u32(lds, c + q + 1u);
+                    const uint32_t v2 = ((by - 0x9Cu) << 8) + (d & 0xFFu) + 156u;
+                    const uint32_t v3 = (d & 0xFFFFu) + ((by - 0xDCu) << 16) + 16540u;
+                    const uint32_t val = by < 0x9Cu ? by : by < 0xDCu ? v2 : by < 0xFCu ? v3 : by == 0xFCu ? (d & 0xFFFFFFu) : d;
+                    exsum += t < cnt ? val : 0u;
+                }
+                const uint32_t e_last = uni(__builtin_amdgcn_readlane(qe, cnt - 1u));
+                found += cnt;
+                vend = c + e_last;
+                sp = e_last >= 64u ? e_last - 64u : e_last;
+                c += e_last >= 64u ? 64u : 0u;
+            }
+        }
+        used = vend + xn - s;
+    }
+    const u32x4 v = unpack256v32_lane(lds, p, b, t);
+    return v.x + v.y + v.z + v.w + 4u + shl32(exsum, b);
+}
+
+
+// phase A with per-run reduction: lane t's partial of block j goes to
+// part[j][t]; after the run lane j sums row j (64 words, 16 ds_read_b128)
+template <uint32_t NC, int MINW, uint32_t kRun>
+__global__ __launch_bounds__(256, MINW) void k_sum_deferred(const VArgs A)
+{
+    __shared__ uint32_t slots[4][kSlotBytes / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t part[4][kRun][64];
+    const uint32_t t = threadIdx.x & 63u;
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    const uint64_t first = (static_cast<uint64_t>(blockIdx.x) * 4u + wv) * kRun;
+    if (first >= A.nblocks)
+        return;
+    uint32_t * slot = slots[wv];
+    const uint64_t in_base = reinterpret_cast<uint64_t>(A.in);
+    const uint32_t n = static_cast<uint32_t>(min_u64(kRun, A.nblocks - first));
+    const bool valid = t < n;
+    const uint64_t o = valid ? A.off[first + t] : 0ull;
+    const uint64_t e = valid ? A.off[first + t + 1u] : 0ull;
+    RunPlaneT<kSlotBytes, true> P;
+    P.init(in_base, in_base + A.in_bytes, o, e, valid);
+    auto issue = [&](Chunk & c, uint32_t jj) { P.template issue<2>(c, jj, t); };
+    auto consume = [&](const Chunk & c, uint32_t jj) {
+        const uint32_t ctl = P.stage(c, jj, slot, t);
+        uint32_t used;
+        part[wv][jj][t] = dsum_partial256v32(slot, (ctl >> kCtlShift) & 15u, t, used);
+        wave_lds_sync();
+    };
+    Chunk C[NC];
+#pragma unroll
+    for (uint32_t u = 0; u + 1 < NC; ++u)
+        issue(C[u], u);
+    bool more = true;
+    for (uint32_t j = 0; more; j += NC)
+    {
+#pragma unroll
+        for (uint32_t u = 0; u < NC; ++u)
+        {
+            if (more)
+            {
+                issue(C[(u + NC - 1) % NC], j + u + NC - 1);
+                consume(C[u], j + u);
+                more = j + u + 1 < n;
+            }
+        }
+    }
+    uint32_t sm = 0u;
+    if (valid)
+    {
+        const u32x4 * row = reinterpret_cast<const u32x4 *>(part[wv][t]);
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i)
+        {
+            const u32x4 q = row[(i + t) & 15u]; // rotated start: lanes hit different banks
+            sm += (q.x + q.y) + (q.z + q.w);
+        }
+        A.out[first + t] = sm;
+    }
+}
+
 // ---- chained-D1 phase A (block delta sums) with another pipeline depth /
 // occupancy / run length: sums[i] = the product's phase A block sum ----------
 template <uint32_t NC, int MINW, uint32_t kRun>
@@ -353,6 +508,14 @@ int launch_sum(const VArgs & A, hipStream_t s)
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+template <uint32_t NC, int MINW, uint32_t kRun>
+int launch_sumd(const VArgs & A, hipStream_t s)
+{
+    const uint32_t grid = static_cast<uint32_t>((A.nblocks + 4u * kRun - 1u) / (4u * kRun));
+    hipLaunchKernelGGL((k_sum_deferred<NC, MINW, kRun>), dim3(grid), dim3(256), 0, s, A);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 } // namespace tpf::dev
 
 // phase A variants: out = u32 block sums
@@ -373,6 +536,9 @@ extern "C" int decvar_sums(int v, const void * in, uint64_t in_bytes, const uint
         case 5: return launch_sum<4, 8, 32>(A, s);
         case 6: return launch_sum<2, 8, 16>(A, s);
         case 7: return launch_sum<12, 4, 16>(A, s);
+        case 8: return launch_sumd<4, 8, 32>(A, s);
+        case 9: return launch_sumd<4, 8, 16>(A, s);
+        case 10: return launch_sumd<6, 7, 16>(A, s);
         default: return -2;
     }
 }
