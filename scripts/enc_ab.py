@@ -45,7 +45,7 @@ def pv(ci, lag, minw, k):
 
 
 VARIANTS = [("twopass", twopass), ("production", pipe), ("tp_nt", probe(13)), ("tp_sc1", probe(14)),
-            ("tp_nt_write", probe(15)), ("lookback", probe(12)), ("lb_k4", probe(5)), ("lb_k6", probe(6)), ("lb_k8", probe(7)),
+            ("tp_nt_write", probe(15)), ("tp_persist8", probe(16)), ("tp_persist4", probe(17)), ("lookback", probe(12)), ("lb_k4", probe(5)), ("lb_k6", probe(6)), ("lb_k8", probe(7)),
             ("lb_k8_a5120", probe(8)), ("lb_k8_a4096", probe(9)), ("lb_k6_a3840", probe(10)), ("lb_k12_a7680", probe(11)),
             ("lb_fallback", probe(4))]
 if os.environ.get("ENC_AB_PIPE"):

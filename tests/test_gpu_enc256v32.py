@@ -129,7 +129,7 @@ def test_full_size_c3_sample_vs_oracle():
     assert torch.equal(out2, vals)
 
 
-@pytest.mark.parametrize("mode", [0, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
+@pytest.mark.parametrize("mode", [0, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17])
 @pytest.mark.parametrize("nb", [1, 31, 33, 1000, 20_000])
 def test_encoder_variants_vs_oracle(mode, nb):
     """Every 256v32 encoder: 0 = production (two-pass), 3 = the two-pass

@@ -950,14 +950,15 @@ hipError_t launch_lb_k(LbCfg c, const uint32_t * in, uint64_t nblocks, const uin
 // plan -> run scan -> write; gate != nullptr: the look-back encoder's fallback
 // (runs only if *gate != 0), launched on a small grid-stride grid
 hipError_t launch_twopass(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, bool d1, uint8_t * out,
-                          uint64_t out_cap, uint64_t * off, void * ws, hipStream_t stream, int probe, const uint32_t * gate)
+                          uint64_t out_cap, uint64_t * off, void * ws, hipStream_t stream, int probe, const uint32_t * gate,
+                          uint32_t per_cu = 8)
 {
     uint32_t * plan = static_cast<uint32_t *>(ws);
     const uint64_t nruns = enc_runs(nblocks);
     const RunScanWs<uint64_t> rs = RunScanWs<uint64_t>::carve(static_cast<uint8_t *>(ws) + al256(nblocks * 4u), nruns);
     const uint64_t per_wg = 4ull * dev::kEncRun;
     const uint64_t full = (nblocks + per_wg - 1) / per_wg;
-    const uint32_t grid = static_cast<uint32_t>(gate ? std::min<uint64_t>(full, grid_cap(stream, 8)) : full);
+    const uint32_t grid = static_cast<uint32_t>(gate ? std::min<uint64_t>(full, grid_cap(stream, per_cu)) : full);
     if (d1)
         hipLaunchKernelGGL(dev::k_enc256v32_plan<true>, dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan, rs.tot,
                            gate);
@@ -1013,6 +1014,7 @@ size_t enc256v32_workspace(uint64_t nblocks)
 //   12 the look-back encoder (kLbK, kLbArena) + its gated two-pass fallback
 //   13 / 14 the two-pass encoder with nt / sc1 value loads in both passes,
 //   15 with nt value loads in the write pass only
+//   16 / 17 the two-pass encoder on a persistent grid-stride grid (8 / 4 WG per CU)
 //   5 / 6 / 7 the look-back encoder with 4 / 6 / 8 blocks per wave in fixed slots,
 //   8 / 9 / 10 / 11 with arenas {8 blocks, 5120 B}, {8, 4096}, {6, 3840}, {12, 7680} (+ fallback)
 //   >= 16 the rejected single-launch pipelined encoder
@@ -1024,6 +1026,20 @@ hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_
         return hipMemsetAsync(off, 0, sizeof(uint64_t), stream);
     if (nblocks + 1 > 0x7FFFFFFFull)
         return hipErrorInvalidValue;
+    if (probe == 16 || probe == 17)
+    {
+        // measurement: the two-pass encoder on a persistent grid-stride grid
+        // (8 / 4 workgroups per CU) instead of one workgroup per 64 blocks;
+        // the gate word is set so the gated kernels run
+        if (ws_bytes < enc256v32_workspace(nblocks))
+            return hipErrorInvalidValue;
+        uint32_t * on = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(ws) + lb_status_bytes(nblocks) - 16u);
+        hipError_t e = hipMemsetAsync(on, 1, 4, stream);
+        if (e != hipSuccess)
+            return e;
+        return launch_twopass(in, nblocks, starts, start0, d1, out, out_cap, off, static_cast<uint8_t *>(ws) + lb_status_bytes(nblocks),
+                              stream, 0, on, probe == 16 ? 8u : 4u);
+    }
     if (probe >= 16)
     {
         // probe >= 16 (measurement): 16 + ci + 1024 * lag + 65536 * minw + 2^20 * per_ticket
