@@ -63,6 +63,17 @@ const unsigned char *tpf_p4D1Dec256v64(const unsigned char *in, unsigned n, uint
  * the previous mode. */
 int tpf_perblock_mode(int mode);
 
+/* Stops the resident block server on every device (the next per-block call
+ * relaunches it).  The server kernel occupies a stream of its own until it
+ * idles out (10 ms without calls), and HIP's hipDeviceSynchronize, hipFree
+ * and hipHostFree wait for every stream of the device: a caller about to do
+ * one of those right after per-block calls calls this first to avoid that
+ * wait.  The library's own frees do so themselves and also hold back other
+ * threads' per-block calls until the free returns.  Mode 0 needs a large BAR
+ * (VRAM mapped into the CPU's address space); without one the server uses the
+ * host-memory mailboxes of mode 2. */
+void tpf_perblock_quiesce(void);
+
 /* ---- stream framing (host, no decoding) -------------------
  * Encoded length of the block at `in` (fmt = TPF_FMT_*, n = values per call),
  * reading at most `avail` bytes; 0 if malformed/truncated.  values_written

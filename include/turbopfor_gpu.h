@@ -111,17 +111,10 @@ int tpf_p4d1enc256v32_batch(const uint32_t *d_in, uint64_t nblocks, const uint32
                             uint8_t *d_out, uint64_t out_cap, uint64_t *d_off, void *d_ws, size_t ws_bytes, void *stream);
 /* Measurement / test hooks (no reference counterpart): mode 1 = the two-pass
  * encoder's plan pass reduced to a wave OR, 2 = its write pass copying the
- * staged values (same loads and stores, output NOT a valid stream); 3 = the
- * two-pass encoder (plan, run scan, write; = tpf_p4enc256v32_batch); 4-12 =
- * the rejected single-pass look-back encoder (valid streams): 4 with its
- * abort word raised before the launch, so its gated two-pass fallback
- * encodes the batch, 5 / 6 / 7 = 4 / 6 / 8 blocks per wave in fixed LDS
- * slots, 8 / 9 / 10 / 11 = per-wave image arenas {8 blocks, 5120 B}, {8,
- * 4096}, {6, 3840}, {12, 7680}, 12 = the default arena {8, 4096} (DESIGN.md
- * 4.4); >= 16 = the rejected
- * single-launch pipelined encoder (a valid stream; 16 + chunk items + 1024 *
- * lag + 65536 * launch-bound waves + 2^20 * entries per ticket, DESIGN.md
- * 4.4; UINT64_MAX in d_off[nblocks] if a bounded wait expired).  Arguments as
+ * staged values (same loads and stores, output NOT a valid stream); 0 / 3 =
+ * the two-pass encoder (plan, run scan, write; = tpf_p4enc256v32_batch).
+ * Other modes: TPF_EINVAL.  (The rejected single-pass encoders of DESIGN.md
+ * 4.4 are not in the library: scripts/enc_variants.hip.)  Arguments as
  * tpf_p4enc256v32_batch. */
 int tpf_probe_enc256v32(int mode, const uint32_t *d_in, uint64_t nblocks, uint8_t *d_out, uint64_t out_cap,
                         uint64_t *d_off, void *d_ws, size_t ws_bytes, void *stream);

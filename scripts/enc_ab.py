@@ -1,8 +1,9 @@
 """A/B of the 256v32 encoders on one box (C4 mix, 10M blocks): the production
 two-pass encoder (batch entry and tpf_probe_enc256v32 mode 3) vs the rejected
-single-pass look-back encoder's variants (modes 4-12), alternating, HIP events on
-the launch stream; every output verified.  ENC_AB_PIPE=1 adds the rejected
-pipelined encoder's variants (modes >= 16)."""
+encoders of scripts/enc_variants.hip (scripts/libencvar.so, built by
+scripts/build_variants.sh: look-back modes 4-12, load policies 13-15,
+persistent grid 16/17), alternating, HIP events on the launch stream; every
+output verified.  ENC_AB_PIPE=1 adds the pipelined encoder's variants."""
 import ctypes
 import os
 import sys
@@ -22,7 +23,12 @@ L = tpf.lib()
 cap = int(L.tpf_p4enc256v32_bound(nb))
 out = torch.empty(cap, dtype=torch.uint8, device=dev)
 offs = torch.empty(nb + 1, dtype=torch.int64, device=dev)
-wsb = int(L.tpf_p4enc256v32_workspace_size(nb))
+V = ctypes.CDLL(os.path.join(ROOT, "scripts", "libencvar.so"))
+V.encvar_workspace_size.restype = ctypes.c_size_t
+V.encvar_workspace_size.argtypes = [ctypes.c_uint64]
+V.encvar_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+wsb = max(int(L.tpf_p4enc256v32_workspace_size(nb)), int(V.encvar_workspace_size(nb)))
 ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
 s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
@@ -33,8 +39,12 @@ def pipe():
 
 def probe(mode):
     def f():
-        assert L.tpf_probe_enc256v32(mode, vals.data_ptr(), nb, out.data_ptr(), cap, offs.data_ptr(), ws.data_ptr(), wsb,
-                                     s) == 0
+        if mode <= 3:
+            assert L.tpf_probe_enc256v32(mode, vals.data_ptr(), nb, out.data_ptr(), cap, offs.data_ptr(), ws.data_ptr(),
+                                         wsb, s) == 0
+        else:
+            assert V.encvar_launch(mode, vals.data_ptr(), nb, out.data_ptr(), cap, offs.data_ptr(), ws.data_ptr(), wsb,
+                                   s) == 0
     return f
 
 

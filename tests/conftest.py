@@ -11,6 +11,8 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device); run with -m gpu")
+    config.addinivalue_line("markers", "variants: measurement tools outside the library (scripts/build_variants.sh); "
+                                       "run with -m variants on a GPU box")
 
 
 def pytest_collection_modifyitems(config, items):

@@ -314,3 +314,65 @@ def test_per_block_server_idle_exit_and_mode_switch():
                 time.sleep(0.05)  # past the server's 10 ms idle exit
     finally:
         L.tpf_perblock_mode(prev)
+
+
+def test_per_block_calls_beside_host_stream_frees(monkeypatch):
+    """a thread making per-block calls (resident server running)
+    while another thread's host-stream calls grow -- i.e. free and reallocate --
+    their staging buffers.  HIP's frees wait for every stream of the device,
+    the server's included; the library stops the server around its own frees
+    and holds back per-block calls meanwhile (tpf::PerblockPause).  Both sides
+    must finish promptly and exactly; tpf_perblock_quiesce() is callable."""
+    import threading
+    import time
+
+    L = capi()
+    L.tpf_p4Enc256v32.restype = ctypes.c_void_p
+    L.tpf_p4Enc256v32.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]
+    L.tpf_p4Dec256v32.restype = ctypes.c_void_p
+    L.tpf_p4Dec256v32.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]
+    L.tpf_host_dec.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                               ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]
+    L.tpf_host_release.restype = None
+    L.tpf_perblock_quiesce.restype = None
+    stop = threading.Event()
+    errors, calls = [], [0]
+    pb = datagen.c2_blocks(16, 11, 10, seed=3)
+
+    def per_block():
+        try:
+            while not stop.is_set():
+                for v in pb:
+                    v = np.ascontiguousarray(v)
+                    buf = np.zeros(4096, np.uint8)
+                    end = L.tpf_p4Enc256v32(v.ctypes.data, 256, buf.ctypes.data)
+                    out = np.zeros(256, np.uint32)
+                    assert L.tpf_p4Dec256v32(buf.ctypes.data, 256, out.ctypes.data) == end
+                    assert np.array_equal(out, v)
+                    calls[0] += 1
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = threading.Thread(target=per_block)
+    th.start()
+    try:
+        t0 = time.time()
+        for k, nb in enumerate((500, 2000, 8000, 500, 16000)):
+            # a growing chunk size makes the pooled pipeline free and reallocate its staging
+            monkeypatch.setenv("TPF_HOST_CHUNK_BYTES", str((64 << 10) * (k + 1)))
+            blocks = np.concatenate([datagen.c2_blocks(nb // 4, bw, 10, seed=k) for bw in (5, 12, 20, 29)])
+            exp_packed, exp_off = oracle_lib.enc256v32_batch(blocks)
+            back = np.zeros_like(blocks)
+            assert L.tpf_host_dec(2, exp_packed.ctypes.data, len(exp_packed), exp_off.ctypes.data, len(blocks), 256,
+                                  back.ctypes.data, None) == 0
+            np.testing.assert_array_equal(back, blocks)
+            if k == 2:
+                L.tpf_host_release()  # frees every pooled pipeline while per-block calls run
+            L.tpf_perblock_quiesce()
+        assert time.time() - t0 < 60
+    finally:
+        stop.set()
+        th.join(timeout=60)
+    assert not th.is_alive()
+    assert not errors, errors
+    assert calls[0] > 0

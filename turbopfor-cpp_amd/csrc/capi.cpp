@@ -225,7 +225,7 @@ int tpf_probe_enc256v32(int mode, const uint32_t * d_in, uint64_t nblocks, uint8
 {
     if (int rc = check_device())
         return rc;
-    if (mode < 1 || !d_off || (nblocks && (!d_in || !d_out || !d_ws)))
+    if (mode < 0 || mode > 3 || !d_off || (nblocks && (!d_in || !d_out || !d_ws)))
         return fail(TPF_EINVAL, "tpf_probe_enc256v32: bad mode or null pointer");
     if (ws_bytes < tpf::enc256v32_workspace(nblocks))
         return fail(TPF_EINVAL, "tpf_probe_enc256v32: workspace too small");

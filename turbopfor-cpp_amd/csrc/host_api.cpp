@@ -28,6 +28,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <shared_mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -179,7 +180,7 @@ struct Server
     // request halves: fine-grained device memory written through the BAR
     // (mode 0; its host and device addresses coincide) and pinned host memory
     // (mode 2)
-    tpf::ServerReq * rq_dev = nullptr;
+    tpf::ServerReq * rq_dev = nullptr; // stays null without a CPU-mapped (large) BAR
     tpf::ServerReq * rq_host = nullptr;
     tpf::ServerReq * rq_host_d = nullptr;
     tpf::ServerAns * an = nullptr;   // answers: coherent pinned host memory (host view)
@@ -208,15 +209,31 @@ struct Server
         an_d = static_cast<tpf::ServerAns *>(dv);
         rq_host = static_cast<tpf::ServerReq *>(pinned(sizeof(tpf::ServerReq), &dv));
         rq_host_d = static_cast<tpf::ServerReq *>(dv);
-        void * q = nullptr;
-        hip_check(hipExtMallocWithFlags(&q, sizeof(tpf::ServerReq), hipDeviceMallocFinegrained), "request mailboxes");
-        hip_check(hipMemsetAsync(q, 0, sizeof(tpf::ServerReq), stream), "request mailboxes");
-        hip_check(hipStreamSynchronize(stream), "request mailboxes");
-        rq_dev = static_cast<tpf::ServerReq *>(q);
+        // Mode 0 writes the request mailboxes in device memory from the CPU,
+        // which needs the whole of VRAM mapped into the CPU's address space
+        // (a large BAR).  Without one the device-memory half is never created
+        // and every call uses the host-memory mailboxes (mode 2's layout).
+        int large_bar = 0;
+        if (hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, dev) != hipSuccess)
+        {
+            large_bar = 0;
+            (void)hipGetLastError();
+        }
+        if (large_bar)
+        {
+            void * q = nullptr;
+            hip_check(hipExtMallocWithFlags(&q, sizeof(tpf::ServerReq), hipDeviceMallocFinegrained), "request mailboxes");
+            hip_check(hipMemsetAsync(q, 0, sizeof(tpf::ServerReq), stream), "request mailboxes");
+            hip_check(hipStreamSynchronize(stream), "request mailboxes");
+            rq_dev = static_cast<tpf::ServerReq *>(q);
+        }
     }
 
     // the request half the current mode uses (host view)
-    tpf::ServerReq * current() const { return g_mode.load(std::memory_order_relaxed) == 2 ? rq_host : rq_dev; }
+    tpf::ServerReq * current() const
+    {
+        return g_mode.load(std::memory_order_relaxed) == 2 || rq_dev == nullptr ? rq_host : rq_dev;
+    }
 
     // caller holds mu, no launch running
     void launch(tpf::ServerReq * rq)
@@ -259,7 +276,8 @@ struct Server
         for (uint32_t i = 0; i < tpf::kServerBoxes; ++i)
         {
             const uint32_t r = reqno[i].load();
-            __atomic_store_n(&rq_dev->box[i].req, r, __ATOMIC_RELAXED);
+            if (rq_dev)
+                __atomic_store_n(&rq_dev->box[i].req, r, __ATOMIC_RELAXED);
             __atomic_store_n(&rq_host->box[i].req, r, __ATOMIC_RELAXED);
         }
         _mm_sfence();
@@ -334,6 +352,14 @@ struct Server
 std::mutex g_srv_mu;
 Server * g_srv[64] = {};
 
+// A resident server kernel keeps its stream busy, and HIP waits for every
+// stream of the device in hipFree / hipHostFree / hipDeviceSynchronize.  So
+// per-block server calls hold g_pause shared, and the library's own frees
+// (host_stream.cpp) hold it exclusively after stopping the servers
+// (tpf::PerblockPause): no server runs during a free and none can be
+// relaunched by another thread's call until the free has returned.
+std::shared_mutex g_pause;
+
 void stop_servers()
 {
     std::lock_guard<std::mutex> g(g_srv_mu);
@@ -376,6 +402,7 @@ struct BoxLease
 
 unsigned char * enc_srv(int fmt, const void * in, unsigned n, unsigned char * out, bool d1, uint64_t start)
 {
+    std::shared_lock<std::shared_mutex> pause(g_pause);
     Server & S = server();
     BoxLease L(S);
     tpf::ServerReqBox * b = L.req();
@@ -404,6 +431,7 @@ const unsigned char * dec_srv(int fmt, const unsigned char * in, unsigned n, voi
     const uint64_t size = tpf_block_size(fmt, in, uint64_t(1) << 20, n, &written);
     if (size == 0 || size > tpf::kServerPayload)
         throw std::runtime_error("turbopfor_amd: malformed P4 block header");
+    std::shared_lock<std::shared_mutex> pause(g_pause);
     Server & S = server();
     BoxLease L(S);
     tpf::ServerReqBox * b = L.req();
@@ -491,7 +519,14 @@ const unsigned char * dec_one(int fmt, const unsigned char * in, unsigned n, voi
 namespace tpf
 {
 void set_last_error(const std::string & msg);
+
+PerblockPause::PerblockPause()
+{
+    g_pause.lock();
+    stop_servers();
 }
+PerblockPause::~PerblockPause() { g_pause.unlock(); }
+} // namespace tpf
 
 namespace
 {
@@ -616,6 +651,12 @@ const unsigned char * p4D1Dec256v64(const unsigned char * in, unsigned n, uint64
 
 // ----------------------------------------------------------- extern "C" mirror
 extern "C" {
+
+void tpf_perblock_quiesce(void)
+{
+    std::lock_guard<std::shared_mutex> g(g_pause);
+    stop_servers();
+}
 
 int tpf_perblock_mode(int mode)
 {

@@ -28,6 +28,7 @@
 
 #include "../../include/turbopfor_capi.h"
 #include "../../include/turbopfor_gpu.h"
+#include "tpf_kernels.h"
 
 namespace tpf
 {
@@ -142,7 +143,10 @@ struct Pin
     ~Pin()
     {
         if (p)
+        {
+            tpf::PerblockPause pause;
             (void)hipHostUnregister(p);
+        }
     }
 };
 
@@ -169,7 +173,10 @@ struct Buf
     void release()
     {
         if (p)
+        {
+            tpf::PerblockPause pause;
             (void)(host ? hipHostFree(p) : hipFree(p));
+        }
         p = nullptr;
         cap = 0;
     }

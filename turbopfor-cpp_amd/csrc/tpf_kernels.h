@@ -9,6 +9,18 @@
 namespace tpf
 {
 
+// Stops the resident per-block servers (host_api.cpp) and keeps them
+// stopped -- no per-block call starts -- while alive: wrap every hipFree /
+// hipHostFree / hipHostUnregister of the library's own buffers in one, since
+// HIP waits for all of the device's streams there, the server's included.
+struct PerblockPause
+{
+    PerblockPause();
+    ~PerblockPause();
+    PerblockPause(const PerblockPause &) = delete;
+    PerblockPause & operator=(const PerblockPause &) = delete;
+};
+
 // Workgroups to launch for a grid-stride kernel: per_cu workgroups on every
 // CU of the current device (cached per device).
 uint64_t grid_cap(hipStream_t stream, uint32_t per_cu);

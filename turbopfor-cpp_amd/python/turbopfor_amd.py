@@ -162,9 +162,8 @@ def probe_hbm(kind, dst, src, nbytes):
 def probe_enc256v32(mode, values, out):
     """Measurement / test hooks of the 256v32 encoder (tpf_probe_enc256v32):
     mode 1 = plan pass as a wave OR, 2 = write pass copying values (not a
-    valid stream); 3 = two-pass encoder, 4 = look-back encoder forced onto its
-    fallback, 5/6/7 = look-back encoder with 4/6/8 blocks per wave (valid
-    streams).  Returns the offsets tensor [nblocks+1]."""
+    valid stream); 0 / 3 = the two-pass encoder.  Returns the offsets tensor
+    [nblocks+1]."""
     import torch
 
     nb = values.numel() // 256
