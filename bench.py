@@ -53,6 +53,9 @@ sys.path.insert(0, os.path.join(ROOT, "turbopfor-cpp_amd", "python"))
 import tpf_shard  # noqa: E402
 import turbopfor_amd as tpf  # noqa: E402
 
+sys.path.insert(0, ROOT)
+import bench_data  # noqa: E402
+
 METRIC = "G int32/s device-resident p4Dec256v32 (+ compressed GB/s vs HBM peak)"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -62,85 +65,72 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def as_i32(v64):
-    """uint32 values held in int64 -> int32 bit patterns."""
-    return (v64 - ((v64 >> 31) << 32)).to(torch.int32)
+# ------------------------------------------------------------ data (GPU)
+# Counter-based generators keyed by the global element index (bench_data.py):
+# every rank holds a slice of ONE global stream.  The thin wrappers keep the
+# signatures the measurement scripts use.
+as_i32 = bench_data.as_i32
 
 
-# --------------------------------------------------------------- data (GPU)
-def gen_c2(nblocks, exc_pct, seed, dev, pcts=None):
-    """[nblocks, 256] uint32 bit patterns: 32 equal segments with bw 1..32,
-    exceptions U[2^bw, 2^32) with probability exc_pct (or pcts cycling per
-    segment) for bw <= 28."""
-    vals = torch.empty((nblocks, 256), dtype=torch.int32, device=dev)
-    seg = [(nblocks * s) // 32 for s in range(33)]
-    g = torch.Generator(device=dev)
-    for s in range(32):
-        bw = s + 1
-        lo, hi = seg[s], seg[s + 1]
-        if hi <= lo:
-            continue
-        pct = pcts[s % len(pcts)] if pcts else exc_pct
-        g.manual_seed(seed * 1000 + bw)
-        n = (hi - lo) * 256
-        v = torch.randint(0, 1 << bw, (n,), device=dev, generator=g, dtype=torch.int64)
-        if pct > 0 and bw <= 28:
-            m = torch.rand(n, device=dev, generator=g) < (pct / 100.0)
-            e = torch.randint(1 << bw, 1 << 32, (n,), device=dev, generator=g, dtype=torch.int64)
-            v = torch.where(m, e, v)
-            del m, e
-        vals[lo:hi] = as_i32(v).view(hi - lo, 256)
-        del v
-    return vals, seg
+def gen_c2(nblocks, exc_pct, seed, dev, pcts=None, first_block=0):
+    return bench_data.gen_c2(nblocks, exc_pct, seed, dev, pcts=pcts, first_block=first_block)
 
 
-def gen_bw(nblocks, bw, exc_pct, seed, dev):
-    """[nblocks, 256] uint32 bit patterns of ONE bit width (C2's per-width
-    generator, benchmarks/ab_test.cpp:1606-1632), generated in 64M-value parts."""
-    vals = torch.empty((nblocks, 256), dtype=torch.int32, device=dev)
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed * 1000 + bw)
-    flat = vals.view(-1)
-    step = 64 << 20
-    for a in range(0, flat.numel(), step):
-        n = min(step, flat.numel() - a)
-        v = torch.randint(0, 1 << bw, (n,), device=dev, generator=g, dtype=torch.int64)
-        if exc_pct > 0 and bw <= 28:
-            m = torch.rand(n, device=dev, generator=g) < (exc_pct / 100.0)
-            e = torch.randint(1 << bw, 1 << 32, (n,), device=dev, generator=g, dtype=torch.int64)
-            v = torch.where(m, e, v)
-            del m, e
-        flat[a:a + n] = as_i32(v)
-        del v
-    return vals
+def gen_bw(nblocks, bw, exc_pct, seed, dev, first_block=0):
+    return bench_data.gen_bw(nblocks, bw, exc_pct, seed, dev, first_block=first_block)
 
 
-def gen_c3(nblocks, seed, dev):
-    """Sorted posting list: 95% gaps bounded Zipf(s=1.1) on [1,64], 5% gaps
-    64+U[0,2^16).  Returns values [nblocks,256] (int32 bit
-    patterns), per-block starts (value preceding each block; 0 for block 0)."""
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed)
-    n = nblocks * 256
-    vals = torch.empty(n, dtype=torch.int32, device=dev)
-    carry = 0
-    step = 64 << 20
-    for a in range(0, n, step):
-        m = min(step, n - a)
-        u = torch.rand(m, device=dev, generator=g, dtype=torch.float64)
-        s = 1.1
-        x = (1.0 + u * (65.0 ** (1 - s) - 1.0)) ** (1.0 / (1 - s))
-        gap = torch.clamp(torch.floor(x), 1, 64).to(torch.int64)
-        big = torch.rand(m, device=dev, generator=g) < 0.05
-        gap = torch.where(big, 64 + torch.randint(0, 1 << 16, (m,), device=dev, generator=g), gap)
-        cs = torch.cumsum(gap, 0) + carry
-        carry = int(cs[-1].item())
-        vals[a : a + m] = as_i32(cs & 0xFFFFFFFF)
-        del u, x, gap, big, cs
-    vals = vals.view(nblocks, 256)
-    starts = torch.zeros(nblocks, dtype=torch.int32, device=dev)
-    starts[1:] = vals[:-1, -1]
-    return vals, starts
+def gen_c3(nblocks, seed, dev, first_block=0, carry_fn=None):
+    return bench_data.gen_c3(nblocks, seed, dev, first_block=first_block, carry_fn=carry_fn)
+
+
+def shard_of(nb, world, rank):
+    """Global block range of this rank: one nb-block shard of the world*nb
+    global stream (tpf_shard.shard_range, weak scaling)."""
+    lo, hi = tpf_shard.shard_range(nb * world, world, rank)
+    assert hi - lo == nb
+    return lo
+
+
+_POPCNT = None
+
+
+def block_mix(packed, offs, chunk=1 << 20):
+    """Header-derived block statistics of a 256v32 stream (SURVEY.md §8 d:
+    "report the header-derived exception fraction on every run"): fraction
+    of vbyte-mode blocks, of bitmap-mode blocks, and exceptions per value
+    (vbyte: the xn byte; bitmap: popcount of the 32-byte bitmap)."""
+    global _POPCNT
+    dev = packed.device
+    if _POPCNT is None or _POPCNT.device != dev:
+        _POPCNT = torch.tensor([bin(i).count("1") for i in range(256)], dtype=torch.int64, device=dev)
+    nb = offs.numel() - 1
+    n_vb = n_bm = exc = 0
+    ar = torch.arange(32, device=dev)
+    for a in range(0, nb, chunk):
+        o = offs[a:min(nb, a + chunk)]
+        h = packed[o].to(torch.int64)
+        x1 = packed[torch.clamp(o + 1, max=packed.numel() - 1)].to(torch.int64)
+        vb = (h & 0xC0) == 0x40
+        bm = ((h & 0xC0) != 0xC0) & ((h & 0x40) == 0) & ((h & 0x80) != 0)
+        n_vb += int(vb.sum().item())
+        n_bm += int(bm.sum().item())
+        exc += int(torch.where(vb, x1, 0).sum().item())
+        ob = o[bm]
+        if ob.numel():
+            idx = torch.clamp(ob.view(-1, 1) + 2 + ar, max=packed.numel() - 1)
+            exc += int(_POPCNT[packed[idx].to(torch.int64)].sum().item())
+    return {"vbyte_block_frac": round(n_vb / max(nb, 1), 4), "bitmap_block_frac": round(n_bm / max(nb, 1), 4),
+            "exception_frac": round(exc / max(nb * 256, 1), 5)}
+
+
+def checksum(t, dev, dist_on):
+    """Sum of the uint32 values (mod 2^64) over all ranks: the decode's
+    checksum of checksums (SURVEY.md §8 e bookkeeping)."""
+    c = (t.view(-1).to(torch.int64) & 0xFFFFFFFF).sum().reshape(1)
+    if dist_on:
+        torch.distributed.all_reduce(c)
+    return int(c.item()) & ((1 << 64) - 1)
 
 
 # --------------------------------------------------------- profile traffic
@@ -517,23 +507,14 @@ def line(metric, value, unit, world, steps, warmup, elapsed, dtype, data, config
 
 
 # ---------------------------------------------------------------- workloads
-def gen_c5(nblocks, exc_pct, seed, dev):
-    """C5 shard (SURVEY.md 8 d: 80M blocks as 8 x 10M shards, bw 8 and 16 at
-    10% exceptions): the first half of the shard's blocks bw 8, the rest bw 16."""
-    h = nblocks // 2
-    vals = torch.empty((nblocks, 256), dtype=torch.int32, device=dev)
-    vals[:h] = gen_bw(h, 8, exc_pct, seed, dev)
-    vals[h:] = gen_bw(nblocks - h, 16, exc_pct, seed, dev)
-    return vals
-
-
 def run_c2(args, world, rank, dev, T, c5=False):
     nb = args.nblocks
     t0 = time.time()
+    first = shard_of(nb, world, rank)
     if c5:
-        vals = gen_c5(nb, args.exc, seed=42 + rank, dev=dev)
+        vals = bench_data.gen_c5(nb, args.exc, seed=42, dev=dev, first_block=first)
     else:
-        vals, seg = gen_c2(nb, args.exc, seed=42 + rank, dev=dev)
+        vals, seg = gen_c2(nb, args.exc, seed=42, dev=dev, first_block=first)
     packed_full, offs = tpf.enc256v32(vals)
     packed = packed_full.clone()
     del packed_full
@@ -547,8 +528,10 @@ def run_c2(args, world, rank, dev, T, c5=False):
     elapsed, kern_ms = T.run(lambda: tpf.dec256v32(packed, offs, nb, out=out), args.steps, args.warmup)
     tpf.dec256v32(packed, offs, nb, out=out, err=err)
     ok = bool(torch.equal(out, vals)) and int(err.item()) == -1
+    sums = {"decoded": checksum(out, dev, T.dist_on), "generated": checksum(vals, dev, T.dist_on)}
     if T.dist_on:
         ok = tpf_shard.all_ok(ok, dev)
+    ok = ok and sums["decoded"] == sums["generated"]
 
     e2e = None
     if args.e2e and rank == 0:
@@ -587,10 +570,12 @@ def run_c2(args, world, rank, dev, T, c5=False):
                         "10% exceptions for bw<=28"),
            "nblocks_per_gpu": nb, "packed_bytes_per_gpu": pbytes, "bytes_per_block": round(pbytes / nb, 1),
            "compressed_GBps": round(pbytes * world / (elapsed / args.steps) / 1e9, 1),
-           "parallelism": f"shard{world}", "verified": ok}
+           "parallelism": f"shard{world}", "shard_blocks": [first, first + nb], "verified": ok,
+           "checksum_all_ranks": sums}
     if e2e:
         cfg["e2e_host_pinned"] = e2e
-    data = (f"synthetic (GPU-generated {'C5' if c5 else 'C2'} values, GPU-encoded; full-size decode verified bit-exact: "
+    data = (f"synthetic (GPU-generated {'C5' if c5 else 'C2'} values: rank r holds blocks [r*nb, (r+1)*nb) of one "
+            "counter-keyed global stream; GPU-encoded; full-size decode verified bit-exact on every rank: "
             + ("ok" if ok else "MISMATCH") + ")")
     return line(METRIC, value, "G int32/s", world, args.steps, args.warmup, elapsed, "u32", data, cfg, roof, cpu), ok
 
@@ -608,7 +593,7 @@ def run_sweep(args, world, rank, dev, T):
     t_start = time.perf_counter()
     ok = True
     for bw in range(1, 33):
-        vals = gen_bw(nb, bw, args.exc, seed=42 + rank, dev=dev)
+        vals = gen_bw(nb, bw, args.exc, seed=42, dev=dev, first_block=shard_of(nb, world, rank))
         packed_full, offs = tpf.enc256v32(vals)
         packed = packed_full.clone()
         del packed_full
@@ -700,22 +685,30 @@ def measure_e2e(packed, offs, nb, vals):
 def run_c3(args, world, rank, dev, T, chained):
     nb = args.nblocks
     t0 = time.time()
-    vals, starts = gen_c3(nb, seed=7 + rank, dev=dev)
+    # ONE posting list over all ranks: rank r holds its blocks [r*nb, (r+1)*nb);
+    # its values continue rank r-1's (the carry is an exclusive prefix of the
+    # shards' gap totals, generation only)
+    first = shard_of(nb, world, rank)
+    carry = (lambda tot: tpf_shard.exclusive_prefix(tot, dev)) if T.dist_on else None
+    vals, starts = gen_c3(nb, seed=7, dev=dev, first_block=first, carry_fn=carry)
     packed_full, offs = tpf.enc256v32(vals, d1=True, starts=starts)
     packed = packed_full.clone()
     del packed_full
     torch.cuda.synchronize()
     pbytes = packed.numel()
-    hdr = packed[offs[:-1]].to(torch.int32) & 0xC0
-    vb_frac = float((hdr == 0x40).float().mean().item())
+    mix = block_mix(packed, offs)
+    vb_frac = mix["vbyte_block_frac"]
     if rank == 0:
         log(f"[bench] c3: {nb} blocks in {time.time() - t0:.1f}s, {pbytes / nb / 256:.3f} B/int, "
-            f"vbyte-mode blocks {vb_frac:.1%}")
+            f"vbyte-mode blocks {vb_frac:.1%}, exception fraction {mix['exception_frac']:.4f}")
     out = torch.empty((nb, 256), dtype=torch.int32, device=dev)
     if chained:
         # phase A (block sums + scan), [all-gather of one u32 per rank], phase B
+        # phase A (block sums + scan), [all-gather of one u32 per rank], phase B.
+        # start0 = the value before the GLOBAL list's first block (0); every
+        # rank's base comes from the exchange, not from its own starts.
         chain = tpf.D1Chain(packed, offs, nb)
-        start0 = int(starts[0].item()) & 0xFFFFFFFF
+        start0 = 0
 
         def step():
             chain.sums()
@@ -726,7 +719,13 @@ def run_c3(args, world, rank, dev, T, chained):
     else:
         fn = lambda: tpf.dec256v32(packed, offs, nb, out=out, starts=starts)
     elapsed, kern_ms = T.run(fn, args.steps, args.warmup)
-    ok = bool(torch.equal(out, vals)) if (not chained or world == 1) else True
+    # every rank checks its slice of the global list (for a chained list this
+    # verifies the cross-rank exchange: a wrong base shifts every value)
+    ok = bool(torch.equal(out, vals))
+    sums = {"decoded": checksum(out, dev, T.dist_on), "generated": checksum(vals, dev, T.dist_on)}
+    if T.dist_on:
+        ok = tpf_shard.all_ok(ok, dev)
+    ok = ok and sums["decoded"] == sums["generated"]
     # data-movement probe of the same stream (decode kernel's loads and stores, no decode)
     _, probe_ms = T.run(lambda: tpf.probe256v32(packed, offs, nb, out), 10, 2)
     avg_ms = float(np.mean(kern_ms))
@@ -748,18 +747,28 @@ def run_c3(args, world, rank, dev, T, chained):
             "per_rank": per_rank}
     cfg = {"workload": "C3: p4D1Dec256v32 " + ("chained list (start0 only)" if chained else "per-block starts")
                        + ", Zipf(1.1) gaps on [1,64] + 5% 64+U[0,2^16)",
-           "nblocks_per_gpu": nb, "bytes_per_int": round(pbytes / nb / 256, 4), "vbyte_block_frac": round(vb_frac, 4),
-           "parallelism": f"shard{world}", "verified": ok}
+           "nblocks_per_gpu": nb, "bytes_per_int": round(pbytes / nb / 256, 4), **mix,
+           "parallelism": f"shard{world}", "shard_blocks": [first, first + nb], "verified": ok,
+           "checksum_all_ranks": sums,
+           "list": "one posting list over all ranks (rank r: blocks [r*nb, (r+1)*nb), values continue rank r-1's)"}
     metric = "G int32/s device-resident p4D1Dec256v32" + (" (chained list)" if chained else "")
     cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_d1(
         packed.cpu().numpy(), offs.cpu().numpy().astype(np.uint64), starts.cpu().numpy().view(np.uint32), nb, chained)
     return line(metric, value, "G int32/s", world, args.steps, args.warmup, elapsed, "u32",
-                "synthetic (GPU-generated posting lists, GPU-encoded)", cfg, roof, cpu), ok
+                "synthetic (GPU-generated posting list, counter-keyed by global position, GPU-encoded; decode verified "
+                "bit-exact on every rank: " + ("ok" if ok else "MISMATCH") + ")", cfg, roof, cpu), ok
 
 
 def run_c4(args, world, rank, dev, T):
+    """BASELINE configs[3]: p4Enc256v32 + p4Dec256v32 round trip (C2 values
+    with the exception rate cycling 0/5/10/25% over the bw segments), then
+    the same round trip in 64 bits: p4Enc256v64 + p4Dec256v64 over nblocks
+    256-value units of bench_data.gen_v64 (bw 1..64, rates 0/5/10/25%,
+    exceptions in 32 bits or above bit 32 in alternate segments:
+    tests/test_p4_64.cpp:587-611).  value = the 32-bit round trip."""
     nb = args.nblocks
-    vals, _ = gen_c2(nb, 0, seed=11 + rank, dev=dev, pcts=[0, 5, 10, 25])
+    first = shard_of(nb, world, rank)
+    vals, _ = gen_c2(nb, 0, seed=11, dev=dev, pcts=[0, 5, 10, 25], first_block=first)
     cap = int(tpf.lib().tpf_p4enc256v32_bound(nb))
     enc_out = torch.empty(cap, dtype=torch.uint8, device=dev)
     dec_out = torch.empty((nb, 256), dtype=torch.int32, device=dev)
@@ -772,67 +781,85 @@ def run_c4(args, world, rank, dev, T):
 
     elapsed, rt_ms = T.run(rt, args.steps, args.warmup)
     ok = bool(torch.equal(dec_out, vals))
-    # 64-bit 256v64 round trip on a quarter of the blocks
-    nb64 = max(1, nb // 4)
-    g = torch.Generator(device=dev)
-    g.manual_seed(5 + rank)
-    bw = torch.randint(1, 65, (nb64, 1), device=dev, generator=g)
-    raw = torch.randint(-(1 << 63), (1 << 63) - 1, (nb64, 256), device=dev, generator=g, dtype=torch.int64)
-    mask = torch.where(bw >= 64, torch.full_like(bw, -1), (torch.ones_like(bw) << bw) - 1)
-    v64 = torch.where(torch.rand((nb64, 256), device=dev, generator=g) < 0.1, raw, raw & mask).contiguous()
-    st64 = {"out": torch.empty(nb64 * 256, dtype=torch.int64, device=dev)}
-
-    def rt64():
-        p, o = tpf.enc_batch("256v64", v64.view(-1), nb64, 256)
-        st64["p"], st64["o"] = p, o
-        tpf.dec_batch("256v64", p, o, nb64, 256, out=st64["out"])
-
-    s64 = max(2, args.steps // 4)
-    el64, _ = T.run(rt64, s64, 1)
-    ok64 = bool(torch.equal(st64["out"].view(nb64, 256), v64))
     # the two halves separately (kernel time, HIP events on the launch stream)
     _, enc_ms = T.run(lambda: tpf.enc256v32(vals, out=enc_out), args.steps, 1)
     _, dec_ms = T.run(lambda: tpf.dec256v32(state["p"], state["o"], nb, out=dec_out), args.steps, 1)
-    out64 = st64["out"]
-    _, enc64_ms = T.run(lambda: tpf.enc_batch("256v64", v64.view(-1), nb64, 256), s64, 1)
-    _, dec64_ms = T.run(lambda: tpf.dec_batch("256v64", st64["p"], st64["o"], nb64, 256, out=out64), s64, 1)
     pbytes = int(state["o"][-1].item())
-    alg_rt = 2 * (nb * (1024 + 8) + pbytes + 8)
-    per_rank = per_rank_stats(world, dev, float(np.mean(rt_ms)), alg_rt / (float(np.mean(rt_ms)) * 1e-3) / 1e9)
+    cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_rt(vals.cpu().numpy().view(np.uint32), nb)
+    del vals, enc_out, dec_out, state
+    torch.cuda.empty_cache()
+
+    # ---- 64-bit leg at the same unit count
+    v64 = bench_data.gen_v64(nb, seed=5, dev=dev, first_block=first)
+    out64 = torch.empty(nb * 256, dtype=torch.int64, device=dev)
+    enc64 = {}
+
+    def enc_64():
+        enc64["p"], enc64["o"] = tpf.enc_batch("256v64", v64.view(-1), nb, 256)
+
+    def rt64():
+        enc_64()
+        tpf.dec_batch("256v64", enc64["p"], enc64["o"], nb, 256, out=out64)
+
+    s64 = max(2, args.steps // 2)
+    el64, rt64_ms = T.run(rt64, s64, 1)
+    ok64 = bool(torch.equal(out64.view(nb, 256), v64))
+    _, enc64_ms = T.run(enc_64, s64, 1)
+    _, dec64_ms = T.run(lambda: tpf.dec_batch("256v64", enc64["p"], enc64["o"], nb, 256, out=out64), s64, 1)
+    p64 = int(enc64["p"].numel())
+    del v64, out64, enc64
+    torch.cuda.empty_cache()
+
+    alg_enc = nb * (1024 + 8) + pbytes + 8
+    alg_dec = pbytes + nb * (1024 + 8) + 8
+    per_rank = per_rank_stats(world, dev, float(np.mean(rt_ms)), (alg_enc + alg_dec) / (float(np.mean(rt_ms)) * 1e-3) / 1e9)
+    ok_all = ok and ok64
+    if T.dist_on:
+        ok_all = tpf_shard.all_ok(ok_all, dev)
     if rank != 0:
         return None
     value = nb * 256 * world / (elapsed / args.steps) / 1e9
     g = lambda n, ms: round(n * 256 / (float(np.mean(ms)) * 1e-3) / 1e9, 2)
-    p64 = int(st64["p"].numel())
-    cfg = {"workload": "C4: p4Enc256v32 + p4Dec256v32 round trip, bw 1..32 segments cycling 0/5/10/25% exceptions",
-           "nblocks_per_gpu": nb, "parallelism": f"shard{world}", "verified": ok,
+    gbs = lambda b, ms: round(b / (float(np.mean(ms)) * 1e-3) / 1e9, 1)
+    a64_enc = nb * (2048 + 8) + p64 + 8
+    a64_dec = p64 + nb * (2048 + 8) + 8
+    cfg = {"workload": "C4: p4Enc256v32 + p4Dec256v32 round trip, bw 1..32 segments cycling 0/5/10/25% exceptions; "
+                       "and p4Enc256v64 + p4Dec256v64 over the same number of 256-value units, bw 1..64 segments "
+                       "cycling 0/5/10/25%, exceptions in 32 bits / above bit 32 in alternate segments",
+           "nblocks_per_gpu": nb, "parallelism": f"shard{world}", "shard_blocks": [first, first + nb],
+           "verified": ok_all, "verified_32": ok, "verified_64": ok64,
            "enc256v32_G_int32_per_s": g(nb, enc_ms), "dec256v32_G_int32_per_s": g(nb, dec_ms),
-           "roundtrip_256v64": {"nblocks": nb64, "G_int64_per_s": round(nb64 * 256 / (el64 / s64) / 1e9, 2),
-                                "enc_G_int64_per_s": g(nb64, enc64_ms), "dec_G_int64_per_s": g(nb64, dec64_ms),
-                                "packed_bytes_per_block": round(p64 / nb64, 1),
-                                "dec_alg_GBps": round((p64 + nb64 * (2048 + 8)) / (float(np.mean(dec64_ms)) * 1e-3) / 1e9, 1),
-                                "verified": ok64}}
+           "bytes_per_block": round(pbytes / nb, 1),
+           "roundtrip_256v64": {"nblocks": nb, "G_int64_per_s": round(nb * 256 / (el64 / s64) / 1e9, 2),
+                                "enc_G_int64_per_s": g(nb, enc64_ms), "dec_G_int64_per_s": g(nb, dec64_ms),
+                                "packed_bytes_per_unit": round(p64 / nb, 1), "verified": ok64}}
     # roofline of the step (encode = plan + offset scan + write launches, then
     # the decode launch, all on the launch stream): algorithmic bytes are the
     # encoder's (1024 in + block out + 8 offset) plus the decoder's (block in
     # + 1024 out + 8 offset) per block; the encoder's second read of the
     # values (plan pass, then write pass) is not counted
-    pbytes = int(state["o"][-1].item())
-    alg_enc = nb * (1024 + 8) + pbytes + 8
-    alg_dec = pbytes + nb * (1024 + 8) + 8
-    gbs = lambda b, ms: round(b / (float(np.mean(ms)) * 1e-3) / 1e9, 1)
     rt_gbs = gbs(alg_enc + alg_dec, rt_ms)
     roof = {"bound": "hbm", "achieved": rt_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(rt_gbs / HBM_PEAK_GBS, 4), **traffic_fields("c4", nb),
             "kernel": "round-trip step: k_enc256v32_plan + run scan (2 small kernels) + k_enc256v32_write + k_dec256v32w<None>",
             "kernel_ms_avg": round(float(np.mean(rt_ms)), 4), "alg_bytes_per_launch": int(alg_enc + alg_dec),
             "alg_bytes_def": "encode: 1024 B values + block bytes + 8 B offset; decode: block bytes + 1024 B + 8 B",
-            "enc_achieved_GBps": gbs(alg_enc, enc_ms), "enc_ms_avg": round(float(np.mean(enc_ms)), 4),
-            "dec_achieved_GBps": gbs(alg_dec, dec_ms), "dec_ms_avg": round(float(np.mean(dec_ms)), 4),
+            "enc_achieved_GBps": gbs(alg_enc, enc_ms), "enc_frac": round(gbs(alg_enc, enc_ms) / HBM_PEAK_GBS, 4),
+            "enc_ms_avg": round(float(np.mean(enc_ms)), 4),
+            "dec_achieved_GBps": gbs(alg_dec, dec_ms), "dec_frac": round(gbs(alg_dec, dec_ms) / HBM_PEAK_GBS, 4),
+            "dec_ms_avg": round(float(np.mean(dec_ms)), 4),
+            "v64": {"kernels": "k_enc128v64_plan + run scan + k_enc128v64_write; k_dec128v64w<2>",
+                    "alg_bytes_def": "encode: 2048 B values + unit bytes + 8 B offset; decode: unit bytes + 2048 B + 8 B",
+                    "rt_achieved_GBps": gbs(a64_enc + a64_dec, rt64_ms),
+                    "rt_frac": round(gbs(a64_enc + a64_dec, rt64_ms) / HBM_PEAK_GBS, 4),
+                    "enc_achieved_GBps": gbs(a64_enc, enc64_ms), "enc_frac": round(gbs(a64_enc, enc64_ms) / HBM_PEAK_GBS, 4),
+                    "enc_ms_avg": round(float(np.mean(enc64_ms)), 4),
+                    "dec_achieved_GBps": gbs(a64_dec, dec64_ms), "dec_frac": round(gbs(a64_dec, dec64_ms) / HBM_PEAK_GBS, 4),
+                    "dec_ms_avg": round(float(np.mean(dec64_ms)), 4), **traffic_fields("c4_64", nb)},
             "per_rank": per_rank}
-    cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_rt(vals.cpu().numpy().view(np.uint32), nb)
     return line("G int32/s device-resident p4Enc256v32+p4Dec256v32 round trip", value, "G int32/s", world, args.steps,
-                args.warmup, elapsed, "u32", "synthetic (GPU-generated)", cfg, roof, cpu), ok and ok64
+                args.warmup, elapsed, "u32", "synthetic (GPU-generated, counter-keyed by global position)", cfg, roof,
+                cpu), ok_all
 
 
 def cpu_abtest_c1(vals_host, blk_host, blen, n):
@@ -868,9 +895,7 @@ def run_c1(args, world, rank, dev, T):
     (tpf_enc_batch / tpf_dec_batch, TPF_FMT_32)."""
     n = 127
     nb = args.nblocks
-    g = torch.Generator(device=dev)
-    g.manual_seed(42 + 8 + n + rank)
-    vals = torch.randint(0, 256, (nb * n,), device=dev, generator=g, dtype=torch.int32)
+    vals = bench_data.gen_c1(nb, n, seed=42, dev=dev, first_block=shard_of(nb, world, rank))
     packed, offs = tpf.enc_batch("32", vals, nb, n)
     out = torch.empty_like(vals)
     elapsed, kern_ms = T.run(lambda: tpf.dec_batch("32", packed, offs, nb, n, out=out), args.steps, args.warmup)

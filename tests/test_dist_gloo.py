@@ -72,6 +72,65 @@ def test_chained_d1_across_two_ranks():
     assert res[0][4] == (0, 300) and res[1][4] == (300, 600)
 
 
+def _global_list_worker(rank, world, port, nb, q):
+    """Rank `rank` of bench.py's multi-GPU C3 path on the CPU: its slice of
+    ONE global posting list (bench_data.gen_c3, carry over earlier ranks by
+    all-gather), chained-D1 encoded (the oracle standing in for the GPU
+    encoder), phase A (block sums), the exchange (tpf_shard.chained_base),
+    phase B -- checked against the generated slice, and the shard's bytes
+    against the global list's encoding cut by shard_range / rebase."""
+    import bench_data
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = tpf_shard.shard_range(world * nb, world, rank)
+        vals, starts = bench_data.gen_c3(hi - lo, 7, "cpu", first_block=lo,
+                                         carry_fn=lambda tot: tpf_shard.exclusive_prefix(tot, "cpu"))
+        v = vals.numpy().view(np.uint32)
+        st = starts.numpy().view(np.uint32)
+        packed, off = oracle_lib.enc256v32_batch(v, starts=st)
+        # phase A: each block's delta total (decode from start 0: last value)
+        raw = oracle_lib.dec256v32_batch(packed, off, hi - lo, starts=np.zeros(hi - lo, np.uint32))
+        sums = raw[:, -1].astype(np.uint64)
+        total = int(sums.sum() & 0xFFFFFFFF)
+        base = tpf_shard.chained_base(torch.tensor([total]), start0=0)
+        pref = np.concatenate([[0], np.cumsum(sums)[:-1]]).astype(np.uint64)
+        got = oracle_lib.dec256v32_batch(packed, off, hi - lo, starts=((pref + base) & 0xFFFFFFFF).astype(np.uint32))
+        ok = bool(np.array_equal(got, v)) and base == int(st[0])
+        # the same slice cut out of the whole list's encoding (one process)
+        gv, gst = bench_data.gen_c3(world * nb, 7, "cpu")
+        gp, goff = oracle_lib.enc256v32_batch(gv.numpy().view(np.uint32), starts=gst.numpy().view(np.uint32))
+        loff, (b0, b1) = tpf_shard.rebase(goff, lo, hi)
+        cut_ok = bool(np.array_equal(gp[b0:b1], packed)) and bool(np.array_equal(loff, off))
+        q.put((rank, ok, cut_ok, tpf_shard.all_ok(ok and cut_ok, "cpu"), base))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_global_posting_list_across_ranks(world):
+    """bench.py's C3 at world > 1 is ONE list: rank r's first value continues
+    rank r-1's last, and the chained decode's cross-rank exchange must rebuild
+    it exactly (the bench used to stitch unrelated lists and skip
+    the check)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_global_list_worker, args=(r, world, port, 40, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(r[1] for r in res), res
+    assert all(r[2] for r in res), res
+    assert all(r[3] for r in res)
+    assert res[0][4] == 0 and all(r[4] != 0 for r in res[1:])
+
+
 def test_shard_range_covers():
     for n in (1, 7, 100, 80_000_000):
         for w in (1, 2, 3, 8):

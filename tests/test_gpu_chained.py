@@ -87,3 +87,43 @@ def test_chained_ws_reuse_and_modes():
     for _ in range(3):
         out = tpf.dec256v32_chained(packed, offs, nb, start0=start0, ws=ws)
         np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), vals)
+
+
+def test_bench_data_same_on_gpu_and_cpu():
+    """bench.py generates on the GPU, the gloo tests on the CPU: the
+    counter-keyed generators give the same integers on both."""
+    import bench_data as B
+
+    for f in (lambda d: B.gen_c2(640, 10, 42, d, first_block=6400)[0],
+              lambda d: B.gen_c5(200, 10, 42, d, first_block=400),
+              lambda d: B.gen_c3(300, 7, d, first_block=300, carry_fn=lambda tot: 123456789)[0],
+              lambda d: B.gen_v64(640, 5, d, first_block=64),
+              lambda d: B.gen_c1(100, 127, 42, d, first_block=7)):
+        assert torch.equal(f("cpu"), f(DEV).cpu())
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("workload", ["c3chain", "c3", "c2"])
+def test_bench_two_ranks_one_gpu(workload, tmp_path):
+    """bench.py --gpus 2 (launcher, two ranks sharing cuda:0 over gloo: RCCL
+    refuses two ranks on one device) on a small shard: rank 1's slice
+    continues rank 0's list, the chained decode's exchange rebuilds it, and
+    the printed `verified` is computed on every rank."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, TPF_BENCH_SAME_GPU="1", TPF_BENCH_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--workload", workload,
+                        "--nblocks", "20000", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-probes"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["verified"] is True
+    assert res["config"]["checksum_all_ranks"]["decoded"] == res["config"]["checksum_all_ranks"]["generated"]
+    assert res["config"]["shard_blocks"] == [0, 20000]

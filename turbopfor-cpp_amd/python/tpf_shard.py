@@ -41,6 +41,17 @@ def chained_base(local_total, start0=0, group=None):
     return (start0 + earlier) & 0xFFFFFFFF
 
 
+def exclusive_prefix(value, device, group=None):
+    """Sum of `value` (a Python int, e.g. a shard's gap total) over the ranks
+    before this one: all-gather of one int64 per rank."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    t = torch.tensor([int(value)], dtype=torch.int64, device=device)
+    gathered = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(gathered, t, group=group)
+    return sum(int(g.item()) for g in gathered[:rank])
+
+
 def max_over_ranks(x, device, group=None):
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
