@@ -792,10 +792,15 @@ def run_c4(args, world, rank, dev, T):
     # ---- 64-bit leg at the same unit count
     v64 = bench_data.gen_v64(nb, seed=5, dev=dev, first_block=first)
     out64 = torch.empty(nb * 256, dtype=torch.int64, device=dev)
+    # encoder output, offsets and workspace allocated once (no allocation in the timed loop)
+    bufs64 = {"out": torch.empty(int(tpf.lib().tpf_enc_bound(tpf.FMT["256v64"], nb, 256)), dtype=torch.uint8, device=dev),
+              "offs": torch.empty(nb + 1, dtype=torch.int64, device=dev),
+              "ws": torch.empty(max(1, int(tpf.lib().tpf_enc_workspace_size(tpf.FMT["256v64"], nb, 256))), dtype=torch.uint8,
+                                device=dev)}
     enc64 = {}
 
     def enc_64():
-        enc64["p"], enc64["o"] = tpf.enc_batch("256v64", v64.view(-1), nb, 256)
+        enc64["p"], enc64["o"] = tpf.enc_batch("256v64", v64.view(-1), nb, 256, **bufs64)
 
     def rt64():
         enc_64()
@@ -807,7 +812,7 @@ def run_c4(args, world, rank, dev, T):
     _, enc64_ms = T.run(enc_64, s64, 1)
     _, dec64_ms = T.run(lambda: tpf.dec_batch("256v64", enc64["p"], enc64["o"], nb, 256, out=out64), s64, 1)
     p64 = int(enc64["p"].numel())
-    del v64, out64, enc64
+    del v64, out64, enc64, bufs64
     torch.cuda.empty_cache()
 
     alg_enc = nb * (1024 + 8) + pbytes + 8

@@ -83,6 +83,11 @@ uint64_t tpf_block_size(int fmt, const uint8_t *in, uint64_t avail, unsigned n, 
 /* Offsets of nblocks consecutive blocks (off[nblocks] = total).  Returns the
  * total byte length, or -(i+1) if block i is malformed/truncated. */
 int64_t tpf_scan_offsets(int fmt, const uint8_t *in, uint64_t in_bytes, unsigned n, uint64_t nblocks, uint64_t *off);
+/* Caller-supplied offsets (off[0..nblocks]): 0 when they never decrease and
+ * off[nblocks] <= in_bytes; -(i+1) when off[i] > off[i+1]; -(nblocks+1) when
+ * the last offset is past in_bytes (-1 for a NULL array).  The host streams
+ * run this before any copy. */
+int64_t tpf_check_offsets(const uint64_t *off, uint64_t nblocks, uint64_t in_bytes);
 
 /* ---- host-memory streams (end-to-end path) ----------------
  * Decode / encode nblocks blocks whose bytes and values live in HOST memory:

@@ -28,6 +28,11 @@ static void st32(uint8_t *p, uint32_t v) { memcpy(p, &v, 4); }
 static void st64(uint8_t *p, uint64_t v) { memcpy(p, &v, 8); }
 
 static uint64_t mask64(unsigned b) { return b >= 64u ? ~0ull : ((1ull << b) - 1ull); }
+/* Exception patch shifts: the reference writes `exc << b`, undefined in C for
+ * b >= the type's width (only reachable from malformed headers); here such a
+ * shift yields 0, as the GPU decoders' shl32 does. */
+static uint32_t shl32u(uint32_t v, unsigned b) { return b >= 32u ? 0u : v << b; }
+static uint64_t shl64u(uint64_t v, unsigned b) { return b >= 64u ? 0u : v << b; }
 
 /* Write the b low bits of v at bit position pos of an LSB-first stream
  * (the buffer must be zero-initialised where bits are written). */
@@ -460,8 +465,9 @@ static const uint8_t *p4dec32_generic(const uint8_t *in, unsigned n, uint32_t *o
         uint32_t v;
         unsigned nbytes = (b + 7u) / 8u;
         if (lay == LAY_H) { /* reads exactly ceil(b/8) bytes, p4dec32.cpp:100-124 */
-            v = 0;
-            for (unsigned i = 0; i < nbytes; ++i) v |= (uint32_t)ip[i] << (8u * i);
+            uint64_t v64 = 0; /* b > 32 is undefined in the reference (p4dec32.cpp:100-116): low 32 bits here */
+            for (unsigned i = 0; i < nbytes; ++i) v64 |= (uint64_t)ip[i] << (8u * i);
+            v = (uint32_t)v64;
         } else {
             v = ld32(ip);
         }
@@ -492,7 +498,7 @@ static const uint8_t *p4dec32_generic(const uint8_t *in, unsigned n, uint32_t *o
             uint64_t word = bm[w];
             while (word) {
                 unsigned bit = (unsigned)__builtin_ctzll(word);
-                out[w * 64u + bit] |= (uint32_t)((uint32_t)exc[k++] << b);
+                out[w * 64u + bit] |= shl32u((uint32_t)exc[k++], b);
                 word &= word - 1ull;
             }
         }
@@ -501,10 +507,11 @@ static const uint8_t *p4dec32_generic(const uint8_t *in, unsigned n, uint32_t *o
     /* vbyte exceptions */
     unsigned xn = *ip++;
     b &= 0x3Fu;
+    if (b > 32u) b = 32u; /* malformed (the reference's unpack is undefined there): clamped as the GPU decoders do */
     ip = unpack_base32(ip, n, out, b, lay);
     uint32_t exc[256 + 64];
     ip = vbdec32(ip, xn, exc);
-    for (unsigned k = 0; k < xn; ++k) out[ip[k]] |= (uint32_t)(exc[k] << b);
+    for (unsigned k = 0; k < xn; ++k) out[ip[k]] |= shl32u(exc[k], b);
     return ip + xn;
 }
 
@@ -683,7 +690,7 @@ const uint8_t *orc_p4dec128v64(const uint8_t *in, unsigned n, uint64_t *out)
             uint64_t word = bm[w];
             while (word) {
                 unsigned bit = (unsigned)__builtin_ctzll(word);
-                out[w * 64u + bit] |= exc[k++] << b;
+                out[w * 64u + bit] |= shl64u(exc[k++], b);
                 word &= word - 1ull;
             }
         }
@@ -695,7 +702,7 @@ const uint8_t *orc_p4dec128v64(const uint8_t *in, unsigned n, uint64_t *out)
     ip = unpack128v64(ip, out, b);
     uint64_t exc[256 + 64];
     ip = vbdec64(ip, xn, exc);
-    for (unsigned k = 0; k < xn; ++k) out[ip[k]] |= exc[k] << b;
+    for (unsigned k = 0; k < xn; ++k) out[ip[k]] |= shl64u(exc[k], b);
     return ip + xn;
 }
 

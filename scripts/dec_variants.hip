@@ -23,6 +23,109 @@
 namespace tpf::dev
 {
 
+// Delta total of one 256v32 D1 block without decoding it: the block's last
+// value minus its start = sum over i of (v[i] + 1) mod 2^32 (applyDelta1_256,
+// p4d1dec256v32_scalar.cpp:39-50).  Exceptions add (sum of ex) << b (a shift
+// left is a multiplication by 2^b, which distributes mod 2^32), so no
+// exception needs its position: no bitmap ranking, no position bytes, no
+// scatter.  Returns the sum (wave-uniform); `used` = consumed bytes.
+// Round 2's phase A block sum, kept here for the round-2 phase-A variants
+// (the library replaced it in round 3: it ADDS exceptions sharing a vbyte
+// position where the reference ORs them; p4_dsum_lanes.h).
+__device__ __forceinline__ uint32_t dsum_block256v32(const uint32_t * lds, uint32_t s, uint32_t t, uint32_t & used)
+{
+    const uint32_t hw = uni(lds_u32(lds, s));
+    const uint32_t h = hw & 0xFFu, x1 = (hw >> 8) & 0xFFu;
+    if ((h & 0xC0u) == 0xC0u)
+    {
+        const uint32_t b = h & 0x3Fu;
+        uint32_t c = uni(lds_u32(lds, s + 1u));
+        if (b < 32u)
+            c &= mask32(b);
+        used = 1u + ((b + 7u) >> 3);
+        return 256u * (c + 1u);
+    }
+    uint32_t exsum = 0u, b, p;
+    if ((h & 0x40u) == 0u)
+    {
+        const uint32_t hdr = (h & 0x80u) ? 2u : 1u;
+        const uint32_t bx = (h & 0x80u) ? min(x1, 32u) : 0u;
+        b = min(h & 0x7Fu, 32u);
+        p = s + hdr;
+        if (bx != 0u)
+        {
+            // xn = popcount of the 256-bit bitmap (lane t reads word t & 7)
+            const uint32_t pc = __builtin_popcount(lds_u32(lds, s + 2u + 4u * (t & 7u)));
+            const uint32_t xn = wave_sum((t < 8u) ? pc : 0u);
+            const uint32_t xs = s + 34u;
+            // uniform trip count, predicated adds: a divergent per-lane loop
+            // costs exec-mask (SALU) work every block, and this pass is bound
+            // by its scalar issue (SQ_INSTS_SALU); lanes past xn
+            // read in-slot bytes and add nothing
+            for (uint32_t k0 = 0; k0 < xn; k0 += kWave)
+            {
+                const uint32_t x = lds_bits(lds, xs * 8u + (k0 + t) * bx, bx);
+                exsum += k0 + t < xn ? x : 0u;
+            }
+            p = xs + ((xn * bx + 7u) >> 3);
+        }
+        used = p + 32u * b - s;
+    }
+    else
+    {
+        b = min(h & 0x3Fu, 32u);
+        const uint32_t xn = x1;
+        p = s + 2u;
+        const uint32_t v0 = p + 32u * b;
+        const uint32_t first = uni(lds_byte(lds, v0));
+        uint32_t vend;
+        if (first == 0xFFu)
+        {
+            for (uint32_t k0 = 0; k0 < xn; k0 += kWave)
+            {
+                const uint32_t x = lds_u32(lds, v0 + 1u + 4u * (k0 + t));
+                exsum += k0 + t < xn ? x : 0u;
+            }
+            vend = v0 + 1u + 4u * xn;
+        }
+        else
+        {
+            // the window walk of vbyte_exceptions, summing instead of storing
+            uint32_t c = v0, sp = 0, found = 0;
+            vend = v0;
+            while (found < xn)
+            {
+                const uint32_t by0 = lds_byte(lds, c + t);
+                const uint32_t len0 = by0 < 0x9Cu ? 1u : by0 < 0xDCu ? 2u : by0 < 0xFCu ? 3u : by0 == 0xFCu ? 4u : 5u;
+                const uint32_t q = window_starts(t + len0, sp, t);
+                const uint32_t m = static_cast<uint32_t>(__builtin_popcountll(__ballot(q < 64u)));
+                const uint32_t cnt = min(m, xn - found);
+                const uint32_t qn = bperm(t + len0, q);
+                const uint32_t qe = q < 64u ? qn : q;
+                {
+                    // every lane decodes (q <= 68: in-slot bytes), lanes >= cnt add nothing
+                    const uint32_t by = lds_byte(lds, c + q);
+                    const uint32_t d = lds_u32(lds, c + q + 1u);
+                    const uint32_t v2 = ((by - 0x9Cu) << 8) + (d & 0xFFu) + 156u;
+                    const uint32_t v3 = (d & 0xFFFFu) + ((by - 0xDCu) << 16) + 16540u;
+                    const uint32_t val = by < 0x9Cu ? by : by < 0xDCu ? v2 : by < 0xFCu ? v3 : by == 0xFCu ? (d & 0xFFFFFFu) : d;
+                    exsum += t < cnt ? val : 0u;
+                }
+                const uint32_t e_last = uni(__builtin_amdgcn_readlane(qe, cnt - 1u));
+                found += cnt;
+                vend = c + e_last;
+                sp = e_last >= 64u ? e_last - 64u : e_last;
+                c += e_last >= 64u ? 64u : 0u;
+            }
+        }
+        used = vend + xn - s;
+    }
+    const u32x4 v = unpack256v32_lane(lds, p, b, t);
+    return wave_sum(v.x + v.y + v.z + v.w + 4u + shl32(exsum, b));
+}
+
+
+
 struct VArgs
 {
     const uint8_t * in;

@@ -127,3 +127,73 @@ def test_bench_two_ranks_one_gpu(workload, tmp_path):
     assert res["n_gpus"] == 2 and res["config"]["verified"] is True
     assert res["config"]["checksum_all_ranks"]["decoded"] == res["config"]["checksum_all_ranks"]["generated"]
     assert res["config"]["shard_blocks"] == [0, 20000]
+
+
+@pytest.mark.parametrize("misalign", [0, 1, 3])
+def test_chained_duplicate_positions(misalign):
+    """A chained list with length-consistent vbyte blocks whose exceptions
+    repeat a position (raw-escape and compressed): the reference ORs them
+    (p4d1dec256v32_scalar.cpp:260; tests/test_oracle_dup_positions.py pins
+    the oracle to it), so every later block's start depends on the OR.
+    Phase A declines such blocks to the wave decoder (p4_dsum_lanes.h)."""
+    import dup_positions
+
+    packed_np, off_np, start0, mod, kinds = dup_positions.dup_list()
+    nb = len(off_np) - 1
+    exp = dup_positions.chained_decode_oracle(packed_np, off_np, nb, start0)
+    buf = torch.zeros(len(packed_np) + 16, dtype=torch.uint8, device=DEV)
+    buf[misalign:misalign + len(packed_np)] = torch.from_numpy(packed_np).to(DEV)
+    packed = buf[misalign:misalign + len(packed_np)]
+    offs = torch.from_numpy(off_np.astype(np.int64)).to(DEV)
+    err = torch.zeros(1, dtype=torch.int64, device=DEV)
+    out = tpf.dec256v32_chained(packed, offs, nb, start0=start0, err=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == -1
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), exp)
+    # per-block starts through the plain D1 decode agree too
+    st = np.concatenate([[start0], exp[:-1, -1]]).astype(np.uint32)
+    o2 = tpf.dec256v32(packed, offs, nb, starts=torch.from_numpy(st.view(np.int32)).to(DEV))
+    np.testing.assert_array_equal(o2.cpu().numpy().view(np.uint32), exp)
+
+
+@pytest.mark.parametrize("maxgap_bits,exc", [(4, 0.0), (9, 0.05), (17, 0.1), (24, 0.3), (31, 0.0)])
+def test_chained_widths_and_big_runs(maxgap_bits, exc):
+    """Phase A across base widths and block sizes: small blocks (many per
+    staging window), runs of ~1 KB blocks (several window passes per run),
+    bitmap and vbyte exceptions, constant blocks; bit-exact vs the oracle's
+    sequential chained decode."""
+    rng = np.random.default_rng(maxgap_bits)
+    nb = 6000
+    bits = rng.integers(0, maxgap_bits + 1, size=(nb, 1))
+    gaps = rng.integers(0, 1 << 62, size=(nb, 256), dtype=np.uint64) & ((np.uint64(1) << bits.astype(np.uint64)) - np.uint64(1))
+    ex = rng.random((nb, 256)) < exc
+    gaps = np.where(ex, rng.integers(0, 1 << 32, size=(nb, 256), dtype=np.uint64) >> np.uint64(1), gaps)
+    gaps[::11] = 0
+    flat = (np.cumsum(gaps.reshape(-1) + np.uint64(1)) + np.uint64(7)) & np.uint64(0xFFFFFFFF)
+    vals = flat.astype(np.uint32).reshape(nb, 256)
+    starts = np.concatenate([[7], vals[:-1, -1]]).astype(np.uint32)
+    packed_np, off_np = oracle_lib.enc256v32_batch(vals, starts=starts)
+    out = tpf.dec256v32_chained(torch.from_numpy(packed_np).to(DEV), torch.from_numpy(off_np.astype(np.int64)).to(DEV), nb,
+                                start0=7)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), vals)
+
+
+def test_chained_random_bytes_with_huge_blocks():
+    """Random bytes cut into blocks of 1 B .. 40 KB (larger than phase A's
+    staging window): no fault, an error is reported, and a clean prefix
+    still decodes exactly."""
+    rng = np.random.default_rng(5)
+    vals, starts = _list(3000, 1, seed=8)
+    packed_np, off_np = oracle_lib.enc256v32_batch(vals, starts=starts)
+    nbad = 2000
+    lens = rng.integers(1, 2400, size=nbad)
+    lens[::50] = rng.integers(16000, 40000, size=len(lens[::50]))
+    garbage = rng.integers(0, 256, size=int(lens.sum()), dtype=np.uint8)
+    allp = np.concatenate([packed_np, garbage])
+    offs = np.concatenate([off_np.astype(np.int64), off_np[-1].astype(np.int64) + np.cumsum(lens)])
+    nb = len(offs) - 1
+    err = torch.zeros(1, dtype=torch.int64, device=DEV)
+    out = tpf.dec256v32_chained(torch.from_numpy(allp).to(DEV), torch.from_numpy(offs).to(DEV), nb, start0=1, err=err)
+    torch.cuda.synchronize()
+    assert 3000 <= int(err.item()) < nb
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32)[:3000], vals)

@@ -52,6 +52,8 @@ uint64_t one_block(int fmt, const uint8_t * in, uint64_t avail, uint32_t n, int 
         uint32_t b = h & 0x3Fu;
         if (wide && b == 63u)
             b = 64u;
+        if (fmt == TPF_FMT_32 && b > 32u) // more than 4 value bytes: undefined in the reference (p4dec32.cpp:100-116)
+            return 0;
         *constant = 1;
         const uint64_t sz = 1u + (b + 7u) / 8u;
         return sz <= avail ? sz : 0;
@@ -87,7 +89,7 @@ uint64_t one_block(int fmt, const uint8_t * in, uint64_t avail, uint32_t n, int 
     uint32_t b = h & 0x3Fu;
     if (wide && b == 63u)
         b = 64u;
-    if (avail < 2)
+    if (b > W || avail < 2) // a 32-bit vbyte block wider than 32 bits: the reference's unpack is undefined there
         return 0;
     const uint32_t xn = in[1];
     uint64_t p = 2u + base_bytes(fmt, n, b);
@@ -150,6 +152,18 @@ uint64_t tpf_block_size(int fmt, const uint8_t * in, uint64_t avail, unsigned n,
         *values_written = static_cast<int>(cst ? n : full);
     }
     return sz;
+}
+
+int64_t tpf_check_offsets(const uint64_t * off, uint64_t nblocks, uint64_t in_bytes)
+{
+    if (!off)
+        return -1;
+    for (uint64_t i = 0; i < nblocks; ++i)
+        if (off[i] > off[i + 1])
+            return -static_cast<int64_t>(i) - 1;
+    if (off[nblocks] > in_bytes)
+        return -static_cast<int64_t>(nblocks) - 1;
+    return 0;
 }
 
 int64_t tpf_scan_offsets(int fmt, const uint8_t * in, uint64_t in_bytes, unsigned n, uint64_t nblocks, uint64_t * off)

@@ -305,11 +305,11 @@ int tpf_host_dec(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_
         else
         {
             // caller-supplied offsets bound every upload: they must rise and stay inside h_in
-            for (uint64_t i = 0; i < nblocks; ++i)
-                if (h_off[i] > h_off[i + 1])
-                    throw Err(TPF_EINVAL, "tpf_host_dec: h_off decreases at block " + std::to_string(i));
-            if (h_off[nblocks] > in_bytes)
+            const int64_t bad = tpf_check_offsets(h_off, nblocks, in_bytes);
+            if (bad == -static_cast<int64_t>(nblocks) - 1)
                 throw Err(TPF_EINVAL, "tpf_host_dec: h_off[nblocks] is past in_bytes");
+            if (bad < 0)
+                throw Err(TPF_EINVAL, "tpf_host_dec: h_off decreases at block " + std::to_string(-bad - 1));
         }
         const size_t es = wide_fmt(fmt) ? 8 : 4;
         const size_t uv = unit_values(fmt, n);

@@ -8,23 +8,28 @@
 // 39% of HBM peak).  The kernel below runs every wave independently with a
 // software pipeline and no workgroup barrier.
 #include "p4_dec_run.h"
+#include "p4_dsum_lanes.h"
 #include "tpf_kernels.h"
 
 #include "p4_scan.h"
 
+#ifndef TPF_DSUM_WINDOW
+#define TPF_DSUM_WINDOW 16384
+#endif
+
 namespace tpf::dev
 {
 
-// blocks per run of the chained decode's phase A (k_dsum256v32w): one run sum
-// each for the run scan; phase B's 16-block runs nest in them
-constexpr uint32_t kSumRun = 32;
+// blocks per run of the chained decode's phase A (k_dsum256v32_lanes): one
+// run sum each for the run scan; phase B's 16-block runs nest in them
+constexpr uint32_t kSumRun = kLaneRun;
 
 enum class StartMode : int
 {
     None = 0,     // p4Dec256v32
     PerBlock = 1, // p4D1Dec256v32, start of block i = starts[i]
     Prefix = 2,   // chained list: start of block i = base + sum of the block sums before i (run scan, p4_scan.h)
-    // 3 was SumOnly (phase A of the chained decode): now k_dsum256v32w
+    // 3 was SumOnly (phase A of the chained decode): now k_dsum256v32_lanes
     Probe = 4,    // measurement only: same loads and stores, no decode (data-movement ceiling)
 };
 
@@ -162,62 +167,223 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
         atomicMin(A.err, static_cast<unsigned long long>(first + stride * __builtin_ctzll(badmask)));
 }
 
-// Phase A of the chained decode as its own kernel: block delta sums
-// (dsum_block256v32, no output, no decode scratch), one sum per kSumRun-block
-// run for the run scan.  Runs of 32 with 4 blocks in flight at 8 waves/SIMD:
-// -4% against 16-block runs with 6 in flight at 7 (scripts/chain_sum_variants.py,
-// same-box A/B of the phase on 10M C3 blocks).
-template <uint32_t NC, int MINW>
-__global__ __launch_bounds__(256, MINW) void k_dsum256v32w(const DecArgs A)
+// Phase A of the chained decode (round 3): the block delta sums of 64-block
+// runs, one lane per block (p4_dsum_lanes.h), one sum per run for the run
+// scan.  A wave stages a run's bytes into its LDS window with coalesced
+// 16-byte loads -- in passes of at most WB bytes starting at the first block
+// not yet summed, each pass summing every block that lies wholly inside it --
+// and the blocks the lane path declines go through the wave decoder one at a
+// time.  Waves walk the runs grid-stride and load the NEXT pass (the same
+// run's next window, or the next run's first) into registers while they sum
+// the current one, so the loads of one pass overlap the arithmetic of the
+// previous (measured without that overlap: staging alone 0.46 ms, staging +
+// sums 1.30 ms per 10M C3 blocks).  Phase B's 16-block runs nest in the
+// 64-block runs.
+#ifdef TPF_DSUM_COUNT
+__device__ unsigned long long g_dsum_count[2]; // blocks sent to the wave decoder, staging passes
+#endif
+
+// One 64-block run of phase A as lanes see it.
+struct DsumRun
 {
-    __shared__ uint32_t slots[4][kSlotBytes / 4];
+    uint64_t first = 0, o = 0, e = 0, rend = 0;
+    uint32_t n = 0, len = 0;
+    bool valid = false, fb = false, done = true;
+
+    __device__ __forceinline__ void load(const DecArgs & A, uint64_t run, uint32_t t, uint32_t wb)
+    {
+        first = run * kLaneRun;
+        n = static_cast<uint32_t>(min_u64(kLaneRun, A.nblocks - first));
+        valid = t < n;
+        o = valid ? A.off[first + t] : 0ull;
+        e = valid ? A.off[first + t + 1u] : 0ull;
+        len = (e >= o && e - o < 0x10000ull) ? static_cast<uint32_t>(e - o) : 0xFFFFFFFFu;
+        // blocks larger than a window (or with implausible offsets) go to the wave decoder
+        fb = valid && (len > wb - 32u || e > A.in_bytes);
+        done = !valid || fb;
+        // end of the run's bytes: a pass never stages past it, so neighbouring
+        // runs do not re-read each other's bytes (offsets ascend in a valid stream)
+        rend = readlane_u64(e, n - 1u);
+    }
+};
+
+// The next staging pass of run R: [wbase, wbase + span) starting at the first
+// block not yet summed (it always fits); false when every block is done.
+template <uint32_t WB>
+__device__ __forceinline__ bool dsum_pass(const DecArgs & A, const DsumRun & R, uint64_t & wbase, uint32_t & span, uint32_t & avail)
+{
+    const uint64_t pend = __ballot(!R.done);
+    if (pend == 0ull)
+        return false;
+    const uint32_t lead = static_cast<uint32_t>(__builtin_ctzll(pend));
+    const uint64_t ws = readlane_u64(R.o, lead);
+    const uint64_t we = readlane_u64(R.e, lead);
+    wbase = ws & ~15ull;
+    span = static_cast<uint32_t>(min_u64(wbase + WB, R.rend > we ? R.rend : we) - wbase);
+    avail = static_cast<uint32_t>(min_u64(sub_sat(A.in_bytes, wbase), WB));
+    return true;
+}
+
+#ifndef TPF_DSUM_WAVES
+#define TPF_DSUM_WAVES 2
+#endif
+template <uint32_t WB>
+__global__ __launch_bounds__(256, TPF_DSUM_WAVES) void k_dsum256v32_lanes(const DecArgs A)
+{
+    static_assert(WB % 1024u == 0u && WB + 64u >= kSlotBytes + 4u * kWaveScratchU32, "the window also hosts the fallback's slot and scratch");
+    constexpr uint32_t NL = WB / 1024u; // 16-byte loads per lane per pass
+    __shared__ uint32_t tab[33 * kSumTabRow];
+    __shared__ __attribute__((aligned(16))) uint32_t win_all[4][(WB + 64u) / 4u];
+    if (threadIdx.x < 33u)
+        build_sum_row(tab + threadIdx.x * kSumTabRow, threadIdx.x);
+    __syncthreads();
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
-    const uint64_t first = (static_cast<uint64_t>(blockIdx.x) * 4u + wv) * kSumRun;
-    if (first >= A.nblocks)
+    const uint64_t nruns = (A.nblocks + kLaneRun - 1u) / kLaneRun;
+    const uint64_t rstride = static_cast<uint64_t>(gridDim.x) * 4u;
+    uint64_t run = static_cast<uint64_t>(blockIdx.x) * 4u + wv;
+    if (run >= nruns)
         return;
-    uint32_t * slot = slots[wv];
+    uint32_t * win = win_all[wv];
     const uint64_t in_base = reinterpret_cast<uint64_t>(A.in);
-    const uint32_t n = static_cast<uint32_t>(min_u64(kSumRun, A.nblocks - first));
-    const bool valid = t < n;
-    const uint64_t o = valid ? A.off[first + t] : 0ull;
-    const uint64_t e = valid ? A.off[first + t + 1u] : 0ull;
-    RunPlaneT<kSlotBytes, true> P;
-    P.init(in_base, in_base + A.in_bytes, o, e, valid);
-    uint32_t sumv = 0u;
-    UsedLanes usedv;
-    auto consume = [&](const Chunk & c, uint32_t jj) {
-        const uint32_t ctl = P.stage(c, jj, slot, t);
-        uint32_t used;
-        const uint32_t sm = dsum_block256v32(slot, (ctl >> kCtlShift) & 15u, t, used);
-        sumv = t == jj ? sm : sumv;
-        wave_lds_sync();
-        usedv.put(used, jj, t);
-    };
-    Chunk C[NC];
+    const uint64_t in_end = in_base + A.in_bytes;
+
+    // the pass in flight: its loads land in r[]
+    u32x4 r[NL];
+    uint64_t wbase = 0;
+    uint32_t span = 0, avail = 0;
+    auto issue = [&]() {
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(A.in + wbase, avail);
 #pragma unroll
-    for (uint32_t u = 0; u + 1 < NC; ++u)
-        P.template issue<2>(C[u], u, t);
-    bool more = true;
-    for (uint32_t j = 0; more; j += NC)
-    {
-#pragma unroll
-        for (uint32_t u = 0; u < NC; ++u)
+        for (uint32_t i = 0; i < NL; ++i)
         {
-            if (more)
+            // unconditional: chunks past the span get an out-of-range offset
+            // (zeros, no traffic); a chunk straddling the end of the stream
+            // reads zeros and is patched byte-wise when staged
+            const uint32_t x = 16u * t + 1024u * i;
+            r[i] = buf_load16(rs, x < span ? x : 0x80000000u);
+        }
+    };
+
+    DsumRun cur;
+    cur.load(A, run, t, WB);
+    uint32_t sumv = 0u;
+    dsum_pass<WB>(A, cur, wbase, span, avail); // the lead lane of a fresh run is pending or every lane declined
+    issue();
+    for (;;)
+    {
+        // ---- stage the pass in flight
+        const uint64_t pbase = wbase;
+        const uint32_t pspan = span;
+#pragma unroll
+        for (uint32_t i = 0; i < NL; ++i)
+        {
+            const uint32_t x = 16u * t + 1024u * i;
+            if (x < pspan)
+                reinterpret_cast<u32x4 *>(win)[x >> 4] = r[i];
+        }
+        {
+            const uint32_t xs = avail & ~15u;
+            if (xs < pspan && (avail & 15u) != 0u && t == ((xs >> 4) & 63u))
+                reinterpret_cast<u32x4 *>(win)[xs >> 4] =
+                    load16_guarded(A.in + pbase, make_rsrc(A.in + pbase, avail), xs, avail);
+        }
+        wave_lds_sync();
+#ifdef TPF_DSUM_COUNT
+        if (t == 0)
+            atomicAdd(&g_dsum_count[1], 1ull);
+#endif
+        const bool in_win = !cur.done && cur.o >= pbase && cur.e <= pbase + pspan;
+        cur.done = cur.done || in_win;
+        // ---- put the next pass in flight: the same run's next window, or the next run's first
+        DsumRun nxt;
+        bool run_end = false, last = false;
+        if (!dsum_pass<WB>(A, cur, wbase, span, avail))
+        {
+            run_end = true;
+            const uint64_t nrun = run + rstride;
+            last = nrun >= nruns;
+            if (!last)
             {
-                P.template issue<2>(C[(u + NC - 1) % NC], j + u + NC - 1, t);
-                consume(C[u], j + u);
-                more = j + u + 1 < n;
+                nxt.load(A, nrun, t, WB);
+                if (!dsum_pass<WB>(A, nxt, wbase, span, avail))
+                    span = 0u; // every block of that run declined: nothing to stage
             }
+            else
+                span = 0u;
+        }
+        if (span != 0u)
+            issue();
+        // ---- sum the staged pass
+        const uint32_t p = in_win ? static_cast<uint32_t>(cur.o - pbase) : 0u;
+        uint32_t s = 0u;
+#ifdef TPF_DSUM_STAGEONLY // measurement builds only (scripts/chain_phase_probe.py)
+        const bool ok = true;
+#else
+        const bool ok = dsum_lanes<WB + 40u>(win, p, cur.len, in_win, tab, s);
+#endif
+        sumv = in_win ? s : sumv;
+        cur.fb = cur.fb || (in_win && !ok);
+        if (!run_end)
+        {
+            wave_lds_sync(); // the window is restaged next
+            continue;
+        }
+        wave_lds_sync();
+        // ---- the run is summed: the declined blocks, one at a time through
+        // the wave decoder (exact: duplicate vbyte positions OR, as in the
+        // reference, and the plain decode's length check); the next pass is in
+        // registers, so the window is free
+        uint64_t fbm = __ballot(cur.fb);
+#ifdef TPF_DSUM_COUNT
+        if (t == 0)
+            atomicAdd(&g_dsum_count[0], static_cast<unsigned long long>(__builtin_popcountll(fbm)));
+#endif
+#ifdef TPF_DSUM_NOFB
+        fbm = 0ull;
+#endif
+        uint64_t badmask = 0ull;
+        uint32_t * slot = win;
+        uint32_t * scr = win + kSlotBytes / 4u;
+        while (fbm != 0ull)
+        {
+            const uint32_t j = static_cast<uint32_t>(__builtin_ctzll(fbm));
+            fbm &= fbm - 1ull;
+            const uint64_t ab = in_base + readlane_u64(cur.o, j);
+            const uint64_t cb = ab & ~15ull;
+            // the plain decode stages at most kSlotBytes - 64 bytes of a block (RunPlaneT)
+            const uint32_t sp = static_cast<uint32_t>(min_u64(sub_sat(in_base + readlane_u64(cur.e, j), cb), kSlotBytes - 64u));
+            const uint32_t av = static_cast<uint32_t>(min_u64(sub_sat(in_end, cb), kSlotBytes));
+            const __amdgpu_buffer_rsrc_t rb = make_rsrc(reinterpret_cast<const void *>(cb), av);
+            for (uint32_t x = 16u * t; x < sp; x += 1024u)
+                reinterpret_cast<u32x4 *>(slot)[x >> 4] = load16_guarded(reinterpret_cast<const uint8_t *>(cb), rb, x, av);
+            wave_lds_sync();
+            const uint32_t sb = static_cast<uint32_t>(ab & 15u);
+            u32x4 v;
+            const uint32_t used = decode_block256v32(slot, sb, uni(lds_u32(slot, sb)), scr, t, v);
+            const uint32_t sm = wave_sum(v.x + v.y + v.z + v.w + 4u);
+            sumv = t == j ? sm : sumv;
+            if (used != rl(cur.len, j))
+                badmask |= 1ull << j;
+            wave_lds_sync();
+        }
+        if (cur.valid)
+            A.sums[cur.first + t] = sumv;
+        publish_run_total(A.run_tot, cur.first / kLaneRun, cur.valid ? sumv : 0u, t);
+        if (A.err != nullptr && t == 0 && badmask != 0ull)
+            atomicMin(A.err, static_cast<unsigned long long>(cur.first + __builtin_ctzll(badmask)));
+        if (last)
+            break;
+        run += rstride;
+        cur = nxt;
+        sumv = 0u;
+        if (span == 0u)
+        {
+            // the new run has nothing to stage (all declined): an empty pass
+            wbase = 0;
+            avail = 0;
         }
     }
-    if (valid)
-        A.sums[first + t] = sumv;
-    publish_run_total(A.run_tot, first / kSumRun, valid ? sumv : 0u, t);
-    const uint64_t badmask = usedv.bad(P.len, valid);
-    if (A.err != nullptr && t == 0 && badmask != 0u)
-        atomicMin(A.err, static_cast<unsigned long long>(first + __builtin_ctzll(badmask)));
 }
 
 } // namespace tpf::dev
@@ -275,6 +441,10 @@ uint64_t chain_runs(uint64_t nblocks) { return (nblocks + dev::kRunDefault - 1u)
 size_t al256(size_t x) { return (x + 255u) & ~size_t(255); }
 } // namespace
 
+// LDS staging window per wave of phase A (bytes)
+constexpr uint32_t kDsumWindow = TPF_DSUM_WINDOW;
+constexpr uint32_t kDsumWgPerCu = (160u * 1024u) / (4u * (kDsumWindow + 64u) + 33u * 64u);
+
 size_t d1chain_workspace(uint64_t nblocks) { return al256(nblocks * 4u) + RunScanWs<uint32_t>::bytes(chain_runs(nblocks)); }
 
 hipError_t launch_d1chain_sums(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, void * ws, size_t ws_bytes,
@@ -288,8 +458,10 @@ hipError_t launch_d1chain_sums(const uint8_t * in, uint64_t in_bytes, const uint
     const RunScanWs<uint32_t> rs = RunScanWs<uint32_t>::carve(static_cast<uint8_t *>(ws) + al256(nblocks * 4u), chain_runs(nblocks));
     dev::DecArgs A{in, in_bytes, off, nblocks, nullptr, nullptr, 0u, sums, err};
     A.run_tot = rs.tot;
+    // grid-stride over the runs: two workgroups per CU (the LDS windows admit two)
     constexpr uint64_t per_wg = 4ull * dev::kSumRun;
-    hipLaunchKernelGGL((dev::k_dsum256v32w<4, 8>), dim3(static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg)), dim3(256), 0, stream, A);
+    const uint64_t wgs = std::min<uint64_t>((nblocks + per_wg - 1) / per_wg, grid_cap(stream, kDsumWgPerCu));
+    hipLaunchKernelGGL((dev::k_dsum256v32_lanes<kDsumWindow>), dim3(static_cast<uint32_t>(wgs)), dim3(256), 0, stream, A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return e;
@@ -309,5 +481,12 @@ hipError_t launch_d1chain_decode(const uint8_t * in, uint64_t in_bytes, const ui
     A.run_tile = rs.tile;
     return launch_mode<dev::StartMode::Prefix>(A, stream);
 }
+
+#ifdef TPF_DSUM_COUNT
+extern "C" int tpf_dsum_counters(unsigned long long * out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(dev::g_dsum_count), 16) == hipSuccess ? 0 : 1;
+}
+#endif
 
 } // namespace tpf

@@ -136,6 +136,19 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t x)
     return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), 63));
 }
 
+__device__ __forceinline__ uint32_t umax32(uint32_t a, uint32_t b) { return a > b ? a : b; }
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x)
+{
+    x = umax32(x, __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false));
+    x = umax32(x, __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false));
+    x = umax32(x, __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false));
+    x = umax32(x, __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false));
+    x = umax32(x, __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false));
+    x = umax32(x, __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false));
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), 63));
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt()
 {
     uint32_t t = lane_id();

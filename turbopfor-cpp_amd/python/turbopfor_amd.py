@@ -215,9 +215,10 @@ def unit_values(fmt, n):
     return _UNIT.get(fmt, n)
 
 
-def enc_batch(fmt, values, nblocks, n, d1=False, starts=None, start0=0):
+def enc_batch(fmt, values, nblocks, n, d1=False, starts=None, start0=0, out=None, offs=None, ws=None):
     """values: int32/int64 CUDA tensor with nblocks*unit_values(fmt, n)
-    elements (bit patterns of uint32/uint64).  Returns (packed, offsets)."""
+    elements (bit patterns of uint32/uint64).  Returns (packed, offsets).
+    out / offs / ws: optional preallocated buffers (reused across calls)."""
     import torch
 
     values = values.contiguous()
@@ -225,10 +226,16 @@ def enc_batch(fmt, values, nblocks, n, d1=False, starts=None, start0=0):
     L = lib()
     f = FMT[fmt]
     cap = int(L.tpf_enc_bound(f, nblocks, n))
-    out = torch.empty(cap, dtype=torch.uint8, device=values.device)
-    offs = torch.empty(nblocks + 1, dtype=torch.int64, device=values.device)
+    if out is None:
+        out = torch.empty(cap, dtype=torch.uint8, device=values.device)
+    assert out.numel() >= cap
+    cap = out.numel()
+    if offs is None:
+        offs = torch.empty(nblocks + 1, dtype=torch.int64, device=values.device)
     wsb = int(L.tpf_enc_workspace_size(f, nblocks, n))
-    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=values.device)
+    if ws is None or ws.numel() < wsb:
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=values.device)
+    wsb = ws.numel()
     rc = L.tpf_enc_batch(f, _ptr(values), nblocks, n, 1 if d1 else 0, _ptr(starts),
                          ctypes.c_uint64(start0 & ((1 << 64) - 1)), _ptr(out), cap, _ptr(offs), _ptr(ws), wsb,
                          _stream(torch))
