@@ -739,7 +739,7 @@ def run_c3(args, world, rank, dev, T, chained):
             "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             **traffic_fields("c3chain" if chained else "c3", nb),
             "kernel_ms_avg": round(avg_ms, 4),
-            "kernel": ("k_dsum256v32w (phase A) + run scan (2 small kernels) + k_dec256v32w<Prefix>" if chained
+            "kernel": ("k_dsum256v32_lanes (phase A) + run scan (2 small kernels) + k_dec256v32w<Prefix>" if chained
                        else "tpf::dev::k_dec256v32w<StartMode::PerBlock>"),
             "probe_GBps": round(probe_alg / (float(np.mean(probe_ms)) * 1e-3) / 1e9, 1),
             "ms_vs_probe": round(avg_ms / float(np.mean(probe_ms)), 3),
@@ -915,7 +915,8 @@ def run_c1(args, world, rank, dev, T):
     value = nb * n * world / (elapsed / args.steps) / 1e9
     roof = {"bound": "hbm", "achieved": round(alg / (avg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), **traffic_fields("c1", nb),
-            "kernel_ms_avg": round(avg_ms, 4), "kernel": "tpf::dev::k_dec_gr<H32> (run-pipelined horizontal p4Dec32 batch)",
+            "kernel_ms_avg": round(avg_ms, 4),
+            "kernel": "tpf::dev::k_dec_pair_h32<false> (two n=127 blocks per wave, one per 32-lane half)",
             "per_rank": per_rank}
     cpu = None
     if not args.no_cpu_baseline and world == 1:

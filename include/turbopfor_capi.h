@@ -68,8 +68,8 @@ int tpf_perblock_mode(int mode);
  * idles out (10 ms without calls), and HIP's hipDeviceSynchronize, hipFree
  * and hipHostFree wait for every stream of the device: a caller about to do
  * one of those right after per-block calls calls this first to avoid that
- * wait.  The library's own frees do so themselves and also hold back other
- * threads' per-block calls until the free returns.  Mode 0 needs a large BAR
+ * wait.  tpf_host_dec / tpf_host_enc / tpf_host_release do so themselves and
+ * hold other threads' per-block calls back until they return.  Mode 0 needs a large BAR
  * (VRAM mapped into the CPU's address space); without one the server uses the
  * host-memory mailboxes of mode 2. */
 void tpf_perblock_quiesce(void);

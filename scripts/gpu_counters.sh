@@ -9,8 +9,8 @@ cd /tmp && export TMPDIR=/tmp
 i=0
 for c in ${COUNTERS:-FETCH_SIZE WRITE_SIZE}; do
   i=$((i+1))
-  timeout -k 10 120 rocprofv3 --pmc ${c//,/ } -d $R/gpurun_out/pmc_$i -o run --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --nblocks ${NB:-2000000} ${BENCH_ARGS} > $R/gpurun_out/pmc_$i.log 2>&1 || { echo "pmc $c rc=$?"; tail -5 $R/gpurun_out/pmc_$i.log; exit 1; }
-  python3 - "$R/gpurun_out/pmc_$i/run_counter_collection.csv" "${KFILTER:-k_dec256v32}" <<'PY'
+  timeout -k 10 120 rocprofv3 --pmc ${c//,/ } -d $R/gpurun_out/pmc_${TAGC:-x}_$i -o run --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --nblocks ${NB:-2000000} ${BENCH_ARGS} > $R/gpurun_out/pmc_${TAGC:-x}_$i.log 2>&1 || { echo "pmc $c rc=$?"; tail -5 $R/gpurun_out/pmc_${TAGC:-x}_$i.log; exit 1; }
+  python3 - "$R/gpurun_out/pmc_${TAGC:-x}_$i/run_counter_collection.csv" "${KFILTER:-k_dec256v32}" <<'PY'
 import csv, sys, collections
 rows = [r for r in csv.DictReader(open(sys.argv[1])) if sys.argv[2] in r['Kernel_Name']]
 agg = collections.defaultdict(list)

@@ -26,15 +26,20 @@ def _dec(mode):
 KERNELS = {
     "c2": ([_dec(0)], "tpf::dev::k_dec256v32w<StartMode::None>"),
     "c3": ([_dec(1)], "tpf::dev::k_dec256v32w<StartMode::PerBlock>"),
-    "c1": ([lambda n: "k_dec_gr" in n and ("FmtE0E" in n or "Fmt)0," in n)], "tpf::dev::k_dec_gr<Fmt::H32>"),
+    "c1": ([lambda n: "k_dec_pair_h32" in n and ("ILb0E" in n or "<false" in n)], "tpf::dev::k_dec_pair_h32<false>"),
     # chained list: phase A (block sums) + phase B (prefix decode); the run
-    # scan between them (p4_scan.hip: 625K u32 run sums, ~5 MB) is not counted
-    "c3chain": ([lambda n: "k_dsum256v32w" in n, _dec(2)], "k_dsum256v32w (phase A) + k_dec256v32w<Prefix>"),
+    # scan between them (p4_scan.hip: 156K u32 run sums, ~1 MB) is not counted
+    "c3chain": ([lambda n: "k_dsum256v32_lanes" in n, _dec(2)], "k_dsum256v32_lanes (phase A) + k_dec256v32w<Prefix>"),
     # round trip: encoder plan + write passes (non-D1) + decode; the run
     # scan between the passes (625K run totals, ~7.5 MB) is not counted
     "c4": ([lambda n: "k_enc256v32_plan" in n and ("ILb0E" in n or "<false" in n),
             lambda n: "k_enc256v32_write" in n and ("ILb0E" in n or "<false" in n), _dec(0)],
            "k_enc256v32_plan<false> + k_enc256v32_write<false> + k_dec256v32w<StartMode::None>"),
+    # C4's 64-bit leg (same rocprof runs as c4): 256v64 encode passes + decode
+    "c4_64": ([lambda n: "k_enc128v64_plan" in n and ("ILj2ELb0E" in n or "<2u, false" in n),
+               lambda n: "k_enc128v64_write" in n and ("ILj2ELb0E" in n or "<2u, false" in n),
+               lambda n: "k_dec128v64w" in n and ("ILj2ELb0E" in n or "<2u, false" in n)],
+              "k_enc128v64_plan<2,false> + k_enc128v64_write<2,false> + k_dec128v64w<2,false>"),
 }
 
 

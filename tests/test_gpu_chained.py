@@ -197,3 +197,27 @@ def test_chained_random_bytes_with_huge_blocks():
     torch.cuda.synchronize()
     assert 3000 <= int(err.item()) < nb
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32)[:3000], vals)
+
+
+@pytest.mark.parametrize("narrow,wide", [(1, 6), (2, 6), (3, 6), (1, 2), (2, 3), (1, 17), (2, 17), (3, 9), (1, 32), (2, 32), (3, 31)])
+def test_chained_mixed_width_runs(narrow, wide):
+    """Phase A sums a wave's lanes with the fold depth of the wave's
+    narrowest block: every run here mixes one or a few narrow blocks (more
+    pre-fold levels) into wide ones, at every lane position."""
+    rng = np.random.default_rng(narrow * 100 + wide)
+    nb = 64 * 6 + 13
+    bits = np.full((nb, 1), wide, dtype=np.uint64)
+    for r in range(nb // 64 + 1):
+        lanes = rng.choice(64, size=1 + r % 3, replace=False)
+        for j in lanes:
+            if r * 64 + j < nb:
+                bits[r * 64 + j, 0] = narrow
+    gaps = rng.integers(0, 1 << 62, size=(nb, 256), dtype=np.uint64) & ((np.uint64(1) << bits) - np.uint64(1))
+    gaps[:, 5] = (np.uint64(1) << bits[:, 0]) - np.uint64(1)  # every block needs exactly its width
+    flat = (np.cumsum(gaps.reshape(-1) + np.uint64(1)) + np.uint64(3)) & np.uint64(0xFFFFFFFF)
+    vals = flat.astype(np.uint32).reshape(nb, 256)
+    starts = np.concatenate([[3], vals[:-1, -1]]).astype(np.uint32)
+    packed_np, off_np = oracle_lib.enc256v32_batch(vals, starts=starts)
+    out = tpf.dec256v32_chained(torch.from_numpy(packed_np).to(DEV), torch.from_numpy(off_np.astype(np.int64)).to(DEV), nb,
+                                start0=3)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), vals)

@@ -31,6 +31,7 @@
 #include <shared_mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/turbopfor.h"
@@ -358,7 +359,24 @@ Server * g_srv[64] = {};
 // (host_stream.cpp) hold it exclusively after stopping the servers
 // (tpf::PerblockPause): no server runs during a free and none can be
 // relaunched by another thread's call until the free has returned.
+// pthread rwlocks prefer readers: a thread issuing per-block calls back to
+// back would starve a pause forever, so a pending pause holds new calls back.
 std::shared_mutex g_pause;
+std::atomic<int> g_pause_waiting{0};
+
+std::shared_lock<std::shared_mutex> perblock_enter()
+{
+    while (g_pause_waiting.load(std::memory_order_acquire) > 0)
+        std::this_thread::yield();
+    return std::shared_lock<std::shared_mutex>(g_pause);
+}
+
+void pause_lock()
+{
+    g_pause_waiting.fetch_add(1, std::memory_order_acq_rel);
+    g_pause.lock();
+    g_pause_waiting.fetch_sub(1, std::memory_order_acq_rel);
+}
 
 void stop_servers()
 {
@@ -402,7 +420,7 @@ struct BoxLease
 
 unsigned char * enc_srv(int fmt, const void * in, unsigned n, unsigned char * out, bool d1, uint64_t start)
 {
-    std::shared_lock<std::shared_mutex> pause(g_pause);
+    const auto pause = perblock_enter();
     Server & S = server();
     BoxLease L(S);
     tpf::ServerReqBox * b = L.req();
@@ -431,7 +449,7 @@ const unsigned char * dec_srv(int fmt, const unsigned char * in, unsigned n, voi
     const uint64_t size = tpf_block_size(fmt, in, uint64_t(1) << 20, n, &written);
     if (size == 0 || size > tpf::kServerPayload)
         throw std::runtime_error("turbopfor_amd: malformed P4 block header");
-    std::shared_lock<std::shared_mutex> pause(g_pause);
+    const auto pause = perblock_enter();
     Server & S = server();
     BoxLease L(S);
     tpf::ServerReqBox * b = L.req();
@@ -522,7 +540,7 @@ void set_last_error(const std::string & msg);
 
 PerblockPause::PerblockPause()
 {
-    g_pause.lock();
+    pause_lock();
     stop_servers();
 }
 PerblockPause::~PerblockPause() { g_pause.unlock(); }
@@ -654,8 +672,9 @@ extern "C" {
 
 void tpf_perblock_quiesce(void)
 {
-    std::lock_guard<std::shared_mutex> g(g_pause);
+    pause_lock();
     stop_servers();
+    g_pause.unlock();
 }
 
 int tpf_perblock_mode(int mode)

@@ -143,10 +143,7 @@ struct Pin
     ~Pin()
     {
         if (p)
-        {
-            tpf::PerblockPause pause;
             (void)hipHostUnregister(p);
-        }
     }
 };
 
@@ -173,10 +170,7 @@ struct Buf
     void release()
     {
         if (p)
-        {
-            tpf::PerblockPause pause;
             (void)(host ? hipHostFree(p) : hipFree(p));
-        }
         p = nullptr;
         cap = 0;
     }
@@ -294,6 +288,10 @@ int tpf_host_dec(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_
         if (nblocks == 0)
             return TPF_OK;
         need_device();
+        // the resident per-block server stays stopped (and per-block calls
+        // wait) for the whole call: HIP's frees, host (un)registrations and
+        // device-wide waits would otherwise wait on the server's stream
+        const tpf::PerblockPause pause;
         std::vector<uint64_t> scanned;
         if (!h_off)
         {
@@ -397,6 +395,7 @@ int tpf_host_enc(int fmt, const void * h_vals, uint64_t nblocks, unsigned n, int
         if (nblocks == 0)
             return TPF_OK;
         need_device();
+        const tpf::PerblockPause pause; // as tpf_host_dec
         const size_t es = wide_fmt(fmt) ? 8 : 4;
         const size_t uv = unit_values(fmt, n);
         const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(nblocks, chunk_value_bytes() / (es * uv)));
@@ -482,6 +481,7 @@ int tpf_host_enc(int fmt, const void * h_vals, uint64_t nblocks, unsigned n, int
 
 void tpf_host_release(void)
 {
+    const tpf::PerblockPause pause; // the frees below wait on every stream of the device
     std::vector<Pipeline *> idle;
     {
         std::lock_guard<std::mutex> g(g_pool_mu);

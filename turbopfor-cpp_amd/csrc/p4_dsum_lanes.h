@@ -77,10 +77,19 @@ __device__ __forceinline__ void build_sum_row(uint32_t * row, uint32_t b)
             row[10 + l] = 0u;
         }
     }
-    row[15] = (b ? 32u % b : 0u) | (levels << 8);
+    // pre levels P: folded per dword before the 8 dwords of a stream word
+    // are added (slots of S = b << P bits then hold sums of 8 dwords: needs
+    // S - b - P >= 3, so P = 3 / 2 / 2 / 1 for b = 1 / 2 / 3 / >= 4); the
+    // top slot [T, 32) may be cut by bit 32, so it is split off and added as
+    // a plain integer (T = start of the slot holding bit 31)
+    const uint32_t pre = min(b == 1u ? 3u : b <= 3u ? 2u : 1u, levels);
+    const uint32_t S = b ? b << pre : 32u;
+    const uint32_t T = S >= 32u ? 0u : S * (31u / S);
+    row[15] = (b ? 32u % b : 0u) | (levels << 8) | (pre << 12) | (T << 16);
 }
 
-__device__ __forceinline__ uint32_t sum_levels(const uint32_t * tab, uint32_t b) { return tab[b * kSumTabRow + 15u] >> 8; }
+__device__ __forceinline__ uint32_t sum_levels(const uint32_t * tab, uint32_t b) { return (tab[b * kSumTabRow + 15u] >> 8) & 15u; }
+__device__ __forceinline__ uint32_t sum_pre(const uint32_t * tab, uint32_t b) { return (tab[b * kSumTabRow + 15u] >> 12) & 15u; }
 
 // Byte / unaligned u32 at LDS byte position pos, the position clamped to the
 // wave's window (lanes without a block, or a malformed header, compute wild
@@ -106,6 +115,83 @@ __device__ __forceinline__ uint32_t wu32(const uint32_t * w, uint32_t pos)
 //   p: the block's byte position in it, len: its length by the offsets,
 //   act: the lane has a block to sum.
 // Returns ok (sum valid); lanes with !ok go to the wave decoder.
+// vbGet32Inline (p4_scalar_internal.h:589-625): byte length and value of a
+// vbyte whose marker is `by` and whose next four bytes are `d`.
+__device__ __forceinline__ uint32_t vb_len32(uint32_t by)
+{
+    return by < 0x9Cu ? 1u : by < 0xDCu ? 2u : by < 0xFCu ? 3u : by == 0xFCu ? 4u : 5u;
+}
+__device__ __forceinline__ uint32_t vb_val32(uint32_t by, uint32_t d)
+{
+    const uint32_t v2 = ((by - 0x9Cu) << 8) + (d & 0xFFu) + 156u;
+    const uint32_t v3 = (d & 0xFFFFu) + ((by - 0xDCu) << 16) + 16540u;
+    return by < 0x9Cu ? by : by < 0xDCu ? v2 : by < 0xFCu ? v3 : by == 0xFCu ? (d & 0xFFFFFFu) : d;
+}
+
+// Base payload sum of one lane's block (see dsum_lanes): P pre levels per
+// dword, L levels in all (per-lane rows whose own counts are smaller hold
+// no-op masks for the extra levels).
+template <uint32_t P, uint32_t L, uint32_t LIM>
+__device__ __forceinline__ uint32_t base_sum_lanes(const uint32_t * w, uint32_t pay, uint32_t b, bool on, uint32_t bmax,
+                                                   const uint32_t * row)
+{
+    const uint32_t meta = row[15];
+    const uint32_t c32 = meta & 0xFFu, pre = (meta >> 12) & 15u, T = meta >> 16;
+    uint32_t PA[P > 0 ? P : 1], PB[P > 0 ? P : 1], QA[L > 0 ? L : 1], QB[L > 0 ? L : 1], W[L > 0 ? L : 1];
+#pragma unroll
+    for (uint32_t l = 0; l < L; ++l)
+    {
+        const uint32_t a = row[l], bb = row[5 + l];
+        W[l] = row[10 + l];
+        if (l < P)
+        {
+            PA[l] = l < pre ? a : 0xFFFFFFFFu;
+            PB[l] = l < pre ? bb : 0u;
+        }
+        QA[l] = l >= pre ? a : 0xFFFFFFFFu;
+        QB[l] = l >= pre ? bb : 0u;
+    }
+    const uint32_t m = pay & 3u;
+    uint32_t q = min(pay, LIM) >> 2;
+    uint32_t phi = 0u, bs = 0u;
+    for (uint32_t k = 0; k < bmax; ++k)
+    {
+        const uint32_t s = phi ? b - phi : 0u;
+        uint32_t d[9];
+#pragma unroll
+        for (uint32_t l = 0; l < 9u; ++l)
+            d[l] = w[q + l];
+        uint32_t firsts = 0u, lo = 0u, hi = 0u;
+#pragma unroll
+        for (uint32_t l = 0; l < 8u; ++l)
+        {
+            const uint32_t x = __builtin_amdgcn_alignbyte(d[l + 1], d[l], m);
+            firsts += __builtin_amdgcn_ubfe(x, 0u, s);
+            uint32_t z = x >> s;
+#pragma unroll
+            for (uint32_t lv = 0; lv < P; ++lv)
+                z = (z & PA[lv]) + ((z >> W[lv]) & PB[lv]);
+            lo += __builtin_amdgcn_ubfe(z, 0u, T);
+            hi += z >> T;
+        }
+        // levels pre..L-1 of each lane: a lane narrower in pre than the
+        // wave's P (e.g. b = 6 beside b = 2) still needs levels pre..P-1
+        // here, so the loop starts at the smallest pre any b < 32 has (1);
+        // QA/QB are no-ops below each lane's own pre
+#pragma unroll
+        for (uint32_t lv = (P < 1u ? P : 1u); lv < L; ++lv)
+            lo = (lo & QA[lv]) + ((lo >> W[lv]) & QB[lv]);
+        bs += on && k < b ? (firsts << phi) + lo + hi : 0u;
+        q = min(q + 8u, LIM / 4u);
+        phi += c32;
+        phi = phi >= b ? phi - b : phi;
+    }
+    return bs;
+}
+
+#ifndef TPF_DSUM_SKIP
+#define TPF_DSUM_SKIP 0 // measurement builds only: 1 base payload, 2 compressed vbyte, 4 raw vbyte, 8 positions
+#endif
 template <uint32_t LIM>
 __device__ __forceinline__ bool dsum_lanes(const uint32_t * w, uint32_t p, uint32_t len, bool act, const uint32_t * tab, uint32_t & sum)
 {
@@ -160,7 +246,7 @@ __device__ __forceinline__ bool dsum_lanes(const uint32_t * w, uint32_t p, uint3
     const bool raw = is_vb && wbyte<LIM>(w, v0) == 0xFFu;
     const bool comp = is_vb && !raw;
     uint32_t vend = v0 + 1u + 4u * xn;
-    if (__ballot(ok && raw) != 0ull)
+    if ((TPF_DSUM_SKIP & 4) == 0 && __ballot(ok && raw) != 0ull)
     {
         // 8 values per step from 9 aligned dwords: one LDS round trip per step
         ok = ok && (!raw || vend + xn - p == len);
@@ -180,15 +266,15 @@ __device__ __forceinline__ bool dsum_lanes(const uint32_t * w, uint32_t p, uint3
                 exsum += on && k0 + u < xn ? __builtin_amdgcn_alignbyte(d[u + 1], d[u], m) : 0u;
         }
     }
-    if (__ballot(ok && comp) != 0ull)
+    if ((TPF_DSUM_SKIP & 2) == 0 && __ballot(ok && comp) != 0ull)
     {
-        // The marker chain is serial; each step reads 24 bytes at c (7 aligned
-        // dwords, realigned to a[0..5] = bytes c..c+23) and decodes up to four
-        // values starting at window offsets <= 15 from registers, so an LDS
-        // round trip serves several values (C3: ~2 bytes per value).
+        // The marker chain is serial.  Each step reads 20 bytes at c (5
+        // aligned dwords, realigned to a[0..3] = bytes c..c+15) and decodes
+        // two values: the first at offset 0 (no selects), the second at the
+        // first one's length (1..5: a one-level select).  Four values per
+        // step cost 2.5x the VALU for under 2x fewer LDS round trips.
         const bool on = ok && comp;
         const uint32_t lim = p + len;
-        const uint32_t kmax = uni(wave_max_u32(on ? xn : 0u));
         uint32_t c = v0, k = 0u;
         bool inb = true;
         for (;;)
@@ -196,44 +282,36 @@ __device__ __forceinline__ bool dsum_lanes(const uint32_t * w, uint32_t p, uint3
             if (__ballot(on && k < xn) == 0ull)
                 break;
             const uint32_t q = min(c, LIM) >> 2, m = c & 3u;
-            uint32_t d[7], a[6];
+            uint32_t d[5], a[4];
 #pragma unroll
-            for (uint32_t u = 0; u < 7u; ++u)
+            for (uint32_t u = 0; u < 5u; ++u)
                 d[u] = w[q + u];
 #pragma unroll
-            for (uint32_t u = 0; u < 6u; ++u)
+            for (uint32_t u = 0; u < 4u; ++u)
                 a[u] = __builtin_amdgcn_alignbyte(d[u + 1], d[u], m);
-            uint32_t o = 0u;
-#pragma unroll
-            for (uint32_t v = 0; v < 4u; ++v)
-            {
-                // x = bytes o..o+3, y = bytes o+4..o+7 (a value is taken only at o <= 15)
-                const uint32_t oc = min(o, 15u);
-                const uint32_t i = oc >> 2, r = oc & 3u;
-                const uint32_t l0 = i == 0u ? a[0] : i == 1u ? a[1] : i == 2u ? a[2] : a[3];
-                const uint32_t l1 = i == 0u ? a[1] : i == 1u ? a[2] : i == 2u ? a[3] : a[4];
-                const uint32_t l2 = i == 0u ? a[2] : i == 1u ? a[3] : i == 2u ? a[4] : a[5];
-                const uint32_t x = __builtin_amdgcn_alignbyte(l1, l0, r);
-                const uint32_t y = __builtin_amdgcn_alignbyte(l2, l1, r);
-                // vbGet32Inline (p4_scalar_internal.h:589-625)
-                const uint32_t by = x & 0xFFu;
-                const uint32_t dd = __builtin_amdgcn_alignbyte(y, x, 1u);
-                const uint32_t v2 = ((by - 0x9Cu) << 8) + (dd & 0xFFu) + 156u;
-                const uint32_t v3 = (dd & 0xFFFFu) + ((by - 0xDCu) << 16) + 16540u;
-                const uint32_t val = by < 0x9Cu ? by : by < 0xDCu ? v2 : by < 0xFCu ? v3 : by == 0xFCu ? (dd & 0xFFFFFFu) : dd;
-                const uint32_t l = by < 0x9Cu ? 1u : by < 0xDCu ? 2u : by < 0xFCu ? 3u : by == 0xFCu ? 4u : 5u;
-                const bool step = on && k < xn && o <= 15u;
-                inb = inb && (!step || c + o < lim);
-                exsum += step ? val : 0u;
-                o += step ? l : 0u;
-                k += step ? 1u : 0u;
-            }
-            c += o;
+            // value 1 at offset 0: marker a0 & 0xFF, data bytes 1..4
+            const uint32_t by1 = a[0] & 0xFFu;
+            const uint32_t dd1 = __builtin_amdgcn_alignbyte(a[1], a[0], 1u);
+            const uint32_t l1 = vb_len32(by1);
+            const bool s1 = on && k < xn;
+            inb = inb && (!s1 || c < lim);
+            exsum += s1 ? vb_val32(by1, dd1) : 0u;
+            // value 2 at offset l1 (1..5): bytes l1..l1+7 from a[i..i+2], i = l1 >> 2
+            const bool hi1 = l1 >= 4u;
+            const uint32_t x0 = hi1 ? a[1] : a[0], x1 = hi1 ? a[2] : a[1], x2 = hi1 ? a[3] : a[2];
+            const uint32_t r = l1 & 3u;
+            const uint32_t xw = __builtin_amdgcn_alignbyte(x1, x0, r), yw = __builtin_amdgcn_alignbyte(x2, x1, r);
+            const uint32_t by2 = xw & 0xFFu;
+            const uint32_t dd2 = __builtin_amdgcn_alignbyte(yw, xw, 1u);
+            const bool s2 = s1 && k + 1u < xn;
+            inb = inb && (!s2 || c + l1 < lim);
+            exsum += s2 ? vb_val32(by2, dd2) : 0u;
+            const uint32_t adv = s1 ? l1 + (s2 ? vb_len32(by2) : 0u) : 0u;
+            c += adv;
+            k += s1 ? (s2 ? 2u : 1u) : 0u;
             // a lane whose walk left its block stops (it is declined below)
-            if (!inb)
-                k = xn;
+            k = inb ? k : xn;
         }
-        (void)kmax;
         vend = comp ? c : vend;
         ok = ok && (!comp || (inb && vend + xn - p == len));
     }
@@ -242,7 +320,7 @@ __device__ __forceinline__ bool dsum_lanes(const uint32_t * w, uint32_t p, uint3
     // reference ORs exceptions that share a position (patch loop
     // p4d1dec256v32_scalar.cpp:260); the wave decoder takes those blocks.
     // 16 positions per step from 5 aligned dwords.
-    if (__ballot(ok && is_vb) != 0ull)
+    if ((TPF_DSUM_SKIP & 8) == 0 && __ballot(ok && is_vb) != 0ull)
     {
         const bool on = ok && is_vb;
         const uint32_t kmax = uni(wave_max_u32(on ? xn : 0u));
@@ -268,50 +346,38 @@ __device__ __forceinline__ bool dsum_lanes(const uint32_t * w, uint32_t p, uint3
         ok = ok && (!is_vb || inc);
     }
 
-    // base payload: per stream word k the 8 dwords share phi = 32k mod b
+    // base payload: per stream word k the 8 dwords share phi = 32k mod b.
+    // Per dword: the first piece (x & mask(s)) << phi is summed raw; the rest
+    // z = x >> s (whole fields from bit 0) is folded `pre` SWAR levels, its
+    // top slot split off; the 8 dwords' folded parts are added, and the sum
+    // folded the remaining levels once per stream word (the fold is linear
+    // while no slot overflows: see build_sum_row).  The level counts are
+    // template parameters: a wave's (max pre, max levels) is always that of
+    // its narrowest block, so six instantiations cover every wave, and the
+    // fold runs exactly its levels (with run-time counts the compiler
+    // if-converts every possible level into selects: 243 VALU per stream
+    // word instead of ~110 at b = 6).
     const bool on = ok && b != 0u;
     const uint32_t bmax = uni(wave_max_u32(on ? b : 0u));
     const uint32_t lmax = uni(wave_max_u32(on ? sum_levels(tab, b) : 0u));
+    const uint32_t pmax = uni(wave_max_u32(on ? sum_pre(tab, b) : 0u));
     uint32_t bs = 0u;
-    if (bmax != 0u)
+    if ((TPF_DSUM_SKIP & 1) == 0 && bmax != 0u)
     {
         const uint32_t * row = tab + (on ? b : 0u) * kSumTabRow;
-        uint32_t A[5], B[5], W[5];
-#pragma unroll
-        for (uint32_t l = 0; l < 5u; ++l)
-        {
-            A[l] = row[l];
-            B[l] = row[5 + l];
-            W[l] = row[10 + l];
-        }
-        const uint32_t c32 = row[15] & 0xFFu;
-        const uint32_t m = pay & 3u;
-        uint32_t q = min(pay, LIM) >> 2;
-        uint32_t prev = w[q];
-        uint32_t phi = 0u;
-        for (uint32_t k = 0; k < bmax; ++k)
-        {
-            const uint32_t s = phi ? b - phi : 0u;
-            uint32_t firsts = 0u, zs = 0u;
-#pragma unroll
-            for (uint32_t l = 0; l < 8u; ++l)
-            {
-                const uint32_t cur = w[q + 1u + l];
-                const uint32_t x = __builtin_amdgcn_alignbyte(cur, prev, m);
-                prev = cur;
-                firsts += __builtin_amdgcn_ubfe(x, 0u, s);
-                uint32_t z = x >> s;
-#pragma unroll
-                for (uint32_t lv = 0; lv < 5u; ++lv)
-                    if (lv < lmax)
-                        z = (z & A[lv]) + ((z >> W[lv]) & B[lv]);
-                zs += z;
-            }
-            bs += on && k < b ? (firsts << phi) + zs : 0u;
-            q = min(q + 8u, LIM / 4u);
-            phi += c32;
-            phi = phi >= b ? phi - b : phi;
-        }
+        const uint32_t key = pmax * 8u + lmax;
+        if (key == 1u * 8u + 3u)
+            bs = base_sum_lanes<1, 3, LIM>(w, pay, b, on, bmax, row);
+        else if (key == 1u * 8u + 2u)
+            bs = base_sum_lanes<1, 2, LIM>(w, pay, b, on, bmax, row);
+        else if (key == 1u * 8u + 1u)
+            bs = base_sum_lanes<1, 1, LIM>(w, pay, b, on, bmax, row);
+        else if (key == 2u * 8u + 4u)
+            bs = base_sum_lanes<2, 4, LIM>(w, pay, b, on, bmax, row);
+        else if (key == 3u * 8u + 5u)
+            bs = base_sum_lanes<3, 5, LIM>(w, pay, b, on, bmax, row);
+        else
+            bs = base_sum_lanes<0, 0, LIM>(w, pay, b, on, bmax, row); // every lane b = 32
     }
     sum = is_const ? 256u * (cv + 1u) : bs + 256u + shl32(exsum, b);
     return ok;
