@@ -268,19 +268,71 @@ __device__ __forceinline__ bool dsum_lanes(const uint32_t * w, uint32_t p, uint3
     }
     if ((TPF_DSUM_SKIP & 2) == 0 && __ballot(ok && comp) != 0ull)
     {
-        // The marker chain is serial.  Each step reads 20 bytes at c (5
-        // aligned dwords, realigned to a[0..3] = bytes c..c+15) and decodes
-        // two values: the first at offset 0 (no selects), the second at the
-        // first one's length (1..5: a one-level select).  Four values per
-        // step cost 2.5x the VALU for under 2x fewer LDS round trips.
-        const bool on = ok && comp;
+        // Fast path, no serial marker chain: when every value is 1 or 2 bytes
+        // (markers < 0xDC; C3's compressed blocks are all of this kind) the
+        // markers of the region follow from the bytes alone.  With A = bytes
+        // in [0x9C, 0xDC) (2-byte markers if they are markers), byte k is a
+        // marker iff byte k-1 is not a marker in A; inside a maximal run of A
+        // bytes the markers alternate from the run's first byte, so they are
+        // the run's bytes of the start's parity, and the byte after a run is
+        // a marker iff the run's last byte is not.  Runs starting at even
+        // offsets are found with one add (A + their start bytes clears them
+        // by carry), all on 0xFF/0x00 byte masks, four bytes per dword.
+        // The region's length comes from the offsets (len - header - base -
+        // xn position bytes); the parse is taken only if it has xn values
+        // that use exactly those bytes, with no marker >= 0xDC.  Sum of the
+        // values = bytes + 255 * (2-byte markers) - (0x9C*256 - 156) * n2.
+        const uint32_t hl = 2u + 32u * b;
+        const uint32_t lr = len - hl - xn;
+        bool fast = ok && comp && len >= hl + xn && lr >= xn && lr <= 64u;
+        if (__ballot(fast) != 0ull)
+        {
+            constexpr uint32_t QMAX = (LIM + 20u) / 4u;
+            const uint32_t jmax = uni(wave_max_u32(fast ? (lr + 3u) >> 2 : 0u));
+            const uint32_t q0 = min(v0, LIM) >> 2, m0 = v0 & 3u;
+            uint32_t dprev = w[q0];
+            uint32_t aprev = 0u, mprev = 0u, cin = 0u, tsum = 0u, s2 = 0u, n1 = 0u, n2 = 0u, bad = 0u;
+            for (uint32_t j = 0; j < jmax; ++j)
+            {
+                const uint32_t dn = w[min(q0 + j + 1u, QMAX)];
+                const uint32_t x = __builtin_amdgcn_alignbyte(dn, dprev, m0); // region bytes 4j..4j+3
+                dprev = dn;
+                const uint32_t rem = lr > 4u * j ? lr - 4u * j : 0u;
+                const uint32_t rm = rem >= 4u ? 0xFFFFFFFFu : mask32(8u * rem);
+                const uint32_t hi = x & 0x80808080u, y = x & 0x7F7F7F7Fu;
+                const uint32_t gedc = (y + 0x24242424u) & hi;                     // bytes >= 0xDC (bit 7)
+                const uint32_t a80 = (y + 0x64646464u) & hi & ~gedc;              // bytes in [0x9C, 0xDC)
+                const uint32_t am = a80 | (a80 - (a80 >> 7));                     // as 0xFF bytes
+                const uint32_t sha = __builtin_amdgcn_alignbyte(am, aprev, 3u);   // A of byte k-1
+                aprev = am;
+                const uint64_t xs = static_cast<uint64_t>(am) + ((am & ~sha) & 0x00010001u) + cin;
+                cin = static_cast<uint32_t>(xs >> 32);
+                const uint32_t re = am & ~static_cast<uint32_t>(xs);              // runs starting at even offsets
+                const uint32_t mr = (re & 0x00FF00FFu) | (am & ~re & 0xFF00FF00u); // markers inside runs
+                const uint32_t shm = __builtin_amdgcn_alignbyte(mr, mprev, 3u);
+                mprev = mr;
+                const uint32_t mk = (mr | ~(am | shm)) & rm;                     // every marker
+                const uint32_t ma = mk & am;
+                tsum = __builtin_amdgcn_sad_u8(x & rm, 0u, tsum);
+                s2 = __builtin_amdgcn_sad_u8(x & ma, 0u, s2);
+                n2 += __builtin_popcount(ma & 0x01010101u);
+                n1 += __builtin_popcount(mk & ~am & 0x01010101u);
+                bad |= mk & gedc;
+            }
+            fast = fast && bad == 0u && n1 + n2 == xn && n1 + 2u * n2 == lr;
+            exsum += fast ? tsum + 255u * s2 - 39780u * n2 : 0u;
+        }
+        // The general walk (any vbyte lengths) for the other lanes.  The
+        // marker chain is serial: each step reads 20 bytes at c (5 aligned
+        // dwords, realigned to a[0..3] = bytes c..c+15) and decodes two
+        // values: the first at offset 0, the second at the first one's
+        // length (1..5: a one-level select).
+        const bool on = ok && comp && !fast;
         const uint32_t lim = p + len;
         uint32_t c = v0, k = 0u;
         bool inb = true;
-        for (;;)
+        while (__ballot(on && k < xn) != 0ull)
         {
-            if (__ballot(on && k < xn) == 0ull)
-                break;
             const uint32_t q = min(c, LIM) >> 2, m = c & 3u;
             uint32_t d[5], a[4];
 #pragma unroll
@@ -303,17 +355,17 @@ __device__ __forceinline__ bool dsum_lanes(const uint32_t * w, uint32_t p, uint3
             const uint32_t xw = __builtin_amdgcn_alignbyte(x1, x0, r), yw = __builtin_amdgcn_alignbyte(x2, x1, r);
             const uint32_t by2 = xw & 0xFFu;
             const uint32_t dd2 = __builtin_amdgcn_alignbyte(yw, xw, 1u);
-            const bool s2 = s1 && k + 1u < xn;
-            inb = inb && (!s2 || c + l1 < lim);
-            exsum += s2 ? vb_val32(by2, dd2) : 0u;
-            const uint32_t adv = s1 ? l1 + (s2 ? vb_len32(by2) : 0u) : 0u;
+            const bool s2v = s1 && k + 1u < xn;
+            inb = inb && (!s2v || c + l1 < lim);
+            exsum += s2v ? vb_val32(by2, dd2) : 0u;
+            const uint32_t adv = s1 ? l1 + (s2v ? vb_len32(by2) : 0u) : 0u;
             c += adv;
-            k += s1 ? (s2 ? 2u : 1u) : 0u;
+            k += s1 ? (s2v ? 2u : 1u) : 0u;
             // a lane whose walk left its block stops (it is declined below)
             k = inb ? k : xn;
         }
-        vend = comp ? c : vend;
-        ok = ok && (!comp || (inb && vend + xn - p == len));
+        vend = comp ? (fast ? v0 + lr : c) : vend;
+        ok = ok && (!comp || fast || (inb && vend + xn - p == len));
     }
     pay = is_vb ? p + 2u : pay;
     // positions must strictly increase for the sum to be exact: the

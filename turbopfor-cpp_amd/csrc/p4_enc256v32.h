@@ -40,7 +40,15 @@ namespace tpf::dev
 
 constexpr uint32_t kImgU32 = 592; // bytes per wave image: 4..7 lead + block (<= 2276 B) + slack, 16-B multiple
 constexpr uint32_t kEncRun = 16;  // blocks per wave run
-constexpr uint32_t kEncNC = 3;    // value chunks in flight per wave (block j+1, j+2 while j is encoded)
+#ifndef TPF_ENC_NC_PLAN
+#define TPF_ENC_NC_PLAN 3
+#endif
+#ifndef TPF_ENC_NC_WRITE
+#define TPF_ENC_NC_WRITE 3
+#endif
+// value chunks in flight per wave (NC: blocks j+1 .. j+NC-1 while j is encoded)
+constexpr uint32_t kEncNCPlan = TPF_ENC_NC_PLAN;
+constexpr uint32_t kEncNCWrite = TPF_ENC_NC_WRITE;
 
 // deltaEnc1 (p4_scalar_internal.h:711-719): d[i] = in[i] - in[i-1] - 1, in[-1] = start.
 __device__ __forceinline__ u32x4 delta_encode(const u32x4 & v, uint32_t start, uint32_t t)
@@ -117,22 +125,22 @@ struct EncRun
     }
 
     // Pipelined walk: body(v, jj) for jj = 0..n-1 with NC blocks in flight.
-    template <int AUX = 0, class Body>
+    template <uint32_t NC, int AUX = 0, class Body>
     __device__ __forceinline__ void walk(uint32_t t, Body && body) const
     {
-        u32x4 C[kEncNC];
+        u32x4 C[NC];
 #pragma unroll
-        for (uint32_t u = 0; u + 1 < kEncNC; ++u)
+        for (uint32_t u = 0; u + 1 < NC; ++u)
             C[u] = load<AUX>(u, t);
         bool more = true;
-        for (uint32_t j = 0; more; j += kEncNC)
+        for (uint32_t j = 0; more; j += NC)
         {
 #pragma unroll
-            for (uint32_t u = 0; u < kEncNC; ++u)
+            for (uint32_t u = 0; u < NC; ++u)
             {
                 if (more)
                 {
-                    C[(u + kEncNC - 1) % kEncNC] = load<AUX>(j + u + kEncNC - 1, t);
+                    C[(u + NC - 1) % NC] = load<AUX>(j + u + NC - 1, t);
                     body(C[u], j + u);
                     more = j + u + 1 < n;
                 }
@@ -158,7 +166,7 @@ __device__ __forceinline__ void plan_run(const EncRun & R, const uint32_t * in, 
     const uint32_t stv = D1 ? R.start_lane(in, starts, start0, t) : 0u;
     szv = 0u;
     pwv = 0u;
-    R.template walk<enc_load_aux(PROBE)>(t, [&](u32x4 v, uint32_t jj) {
+    R.template walk<kEncNCPlan, enc_load_aux(PROBE)>(t, [&](u32x4 v, uint32_t jj) {
         if constexpr (D1)
             v = delta_encode(v, rl32(stv, jj), t);
         Plan32 P;
@@ -185,7 +193,7 @@ __device__ __forceinline__ void write_run(const EncRun & R, const uint32_t * in,
                                           uint32_t * val, uint64_t out_base, uint64_t cap_end, uint32_t t)
 {
     const uint32_t stv = D1 ? R.start_lane(in, starts, start0, t) : 0u;
-    R.template walk<enc_load_aux(PROBE)>(t, [&](u32x4 v, uint32_t jj) {
+    R.template walk<kEncNCWrite, enc_load_aux(PROBE)>(t, [&](u32x4 v, uint32_t jj) {
         if constexpr (D1)
             v = delta_encode(v, rl32(stv, jj), t);
         const uint32_t size = rl32(szv, jj);
