@@ -140,3 +140,67 @@ def test_p4dec32_corrupt_offsets_reported(n):
     torch.cuda.synchronize()
     assert int(err.item()) == -1  # UINT64_MAX: every block consistent
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32).reshape(nb, n), vals)
+
+
+def _h32_values(rng, nb, n):
+    """Blocks that exercise every p4Dec32 mode the windowed decoder parses:
+    constant, plain, bitmap and vbyte exceptions (raw and compressed), at base
+    widths 0..32 -- runs of small blocks share one staged window, 1 KB blocks
+    split runs into windows of two."""
+    bw = rng.integers(0, 33, size=(nb, 1)).astype(np.uint64)
+    vals = rng.integers(0, 1 << 62, size=(nb, n), dtype=np.uint64) & ((np.uint64(1) << bw) - np.uint64(1))
+    rate = rng.choice([0.0, 0.02, 0.1, 0.3], size=(nb, 1))
+    exc = rng.random((nb, n)) < rate
+    big = rng.integers(0, 1 << 32, size=(nb, n), dtype=np.uint64) >> rng.integers(0, 24, size=(nb, 1)).astype(np.uint64)
+    vals = np.where(exc, big, vals).astype(np.uint32)
+    const = rng.random(nb) < 0.1
+    vals[const] = vals[const, :1]
+    return vals
+
+
+@pytest.mark.parametrize("n", [1, 33, 64, 65, 127, 128, 129, 255, 256])
+@pytest.mark.parametrize("d1", [False, True])
+def test_p4dec32_windows_vs_oracle(n, d1):
+    """k_dec_h32w (p4Dec32 / p4D1Dec32 batches, n <= 256): mixed modes and
+    widths over 64-block wave runs and their staging windows, ragged last run
+    (nb % 64 != 0), bit-exact against the oracle's decode of the oracle's
+    encoding (reference src/scalar/p4dec32.cpp:70-142, p4d1dec32.cpp)."""
+    rng = np.random.default_rng(1000 * n + d1)
+    nb = 3001
+    vals = _h32_values(rng, nb, n)
+    starts = rng.integers(0, 1 << 32, size=nb, dtype=np.uint64).astype(np.uint32) if d1 else None
+    if d1:
+        # p4D1Enc32 codes vals as strictly increasing deltas from the start
+        vals = (np.cumsum(vals.astype(np.uint64) + 1, axis=1) + starts[:, None].astype(np.uint64) - 1).astype(np.uint32)
+    packed, off = oracle_lib.enc32_batch(vals, starts=starts)
+    exp = oracle_lib.dec32_batch(packed, off, nb, n, starts=starts)
+    np.testing.assert_array_equal(exp, vals)
+    err = torch.zeros(1, dtype=torch.int64, device=DEV)
+    out = tpf.dec_batch("32", torch.from_numpy(packed).to(DEV), torch.from_numpy(off.astype(np.int64)).to(DEV), nb, n,
+                        starts=to_dev(starts, False) if d1 else None, err=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == -1
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32).reshape(nb, n), vals)
+
+
+def test_p4dec32_windows_oversize_block_reported():
+    """An offset pair that claims more bytes than a staging window (or runs
+    past the stream) is reported through d_err, blocks before it stay exact."""
+    rng = np.random.default_rng(5)
+    nb, n = 200, 127
+    vals = rng.integers(0, 1 << 9, size=(nb, n), dtype=np.uint64).astype(np.uint32)
+    packed, off = oracle_lib.enc32_batch(vals)
+    pad = np.zeros(len(packed) + 8192, dtype=np.uint8)
+    pad[: len(packed)] = packed
+    bad = off.astype(np.int64).copy()
+    bad[71:] += 4000  # block 70 claims 4000 extra bytes
+    err = torch.zeros(1, dtype=torch.int64, device=DEV)
+    out = tpf.dec_batch("32", torch.from_numpy(pad).to(DEV), torch.from_numpy(bad).to(DEV), nb, n, err=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 70
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32).reshape(nb, n)[:70], vals[:70])
+    err.zero_()
+    short = torch.from_numpy(packed[: int(off[150])].copy()).to(DEV)  # stream ends at block 150
+    tpf.dec_batch("32", short, torch.from_numpy(off.astype(np.int64)).to(DEV), nb, n, err=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 150

@@ -117,6 +117,200 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void k_de
         atomicMin(err, static_cast<unsigned long long>(first + __builtin_ctzll(badmask)));
 }
 
+// ---- p4Dec32 / p4D1Dec32 batches (n <= 256): windows staged whole ---------
+// C1 (BASELINE configs[0]) is n = 127: 128-byte blocks for 508 B of output.
+// k_dec_gr stages and parses every block on its own -- per block a run-plane
+// lookup, a staging round trip and the header logic on the scalar unit
+// (counters: 100 SALU, 24 branches, 41 VALU per block; the CU's one scalar
+// unit bounds it).  Here a wave owns 64 consecutive blocks and stages a
+// WINDOW of them at once: every block that ends inside kHWin bytes from the
+// 16-aligned start of the first one, with full-wave 16-byte loads; then lane
+// j parses block j's header in vector registers (mode, base width, payload
+// offset, bitmap exception count, consumed bytes -- one instruction stream
+// for the whole window) and the blocks are unpacked one after the other with
+// a single v_readlane of the packed header word each.  Blocks with vbyte
+// exceptions go through decode_block_g (p4_generic.h) from the same window.
+// The length check is lane-held: one compare and one ballot per run.
+// Reference: src/scalar/p4dec32.cpp:70-142 (p4Dec32), p4d1dec32.cpp.
+constexpr uint32_t kHRun = 64;   // blocks per wave
+// store cache policy of the values (A/B knob).  A block's 508 B start at any
+// dword, so a store instruction covers parts of three 128-B lines: default
+// write-back stores let L2 merge them (C1, A/B on one box: 900-907 G int32/s)
+// where nt stores ran 632-659 and "sc1 nt" (write-through) 412-416.
+#ifndef TPF_H32_STORE_AUX
+#define TPF_H32_STORE_AUX 0
+#endif
+constexpr uint32_t kHWin = 2560; // window staging bytes per wave (p4Enc32 blocks of n <= 256 values are about 1 KB at most)
+
+// lane-parsed header word: [0,12) payload byte in the window (vbyte: block
+// byte), [12,18) b, [18,20) kind, [20,26) bx
+enum : uint32_t
+{
+    kH32Plain = 0,
+    kH32Bitmap = 1,
+    kH32Vbyte = 2,
+    kH32Const = 3,
+};
+
+// bitmap words of an n-bit bitmap at window byte s (bits past n cleared)
+__device__ __forceinline__ void h32_bitmap(const uint32_t * slot, uint32_t s, uint32_t n, uint64_t bm[4], uint32_t pc[4])
+{
+    const uint32_t words = (n + 63u) >> 6;
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u)
+    {
+        uint64_t w = u < words ? lds_u64(slot, s + 8u * u) : 0ull;
+        if (u == words - 1u && (n & 63u))
+            w &= (1ull << (n & 63u)) - 1ull;
+        bm[u] = w;
+        pc[u] = static_cast<uint32_t>(__builtin_popcountll(w));
+    }
+}
+
+template <bool D1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void k_dec_h32w(const uint8_t * __restrict in, uint64_t in_bytes, const uint64_t * __restrict off,
+                                                   uint64_t nblocks, uint32_t n, uint32_t * __restrict out,
+                                                   const uint32_t * __restrict starts, unsigned long long * __restrict err)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t slots[4][kHWin / 4 + 4]; // +16 B: lds_u32 reads past a window's end
+    __shared__ uint32_t scratch[4][512];
+    const uint32_t t = threadIdx.x & 63u;
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    uint32_t * slot = slots[wv];
+    const uint64_t first = (static_cast<uint64_t>(blockIdx.x) * 4u + wv) * kHRun;
+    if (first >= nblocks)
+        return;
+    const uint32_t nr = static_cast<uint32_t>(min_u64(kHRun, nblocks - first));
+    const bool valid = t < nr;
+    const uint64_t o = valid ? off[first + t] : 0ull;
+    const uint64_t e = valid ? off[first + t + 1u] : 0ull;
+    // plausible blocks only: inside the stream and at most a window minus its phase
+    const uint32_t len = (valid && e >= o && e <= in_bytes && e - o <= kHWin - 16u) ? static_cast<uint32_t>(e - o) : 0xFFFFFFFFu;
+    const uint32_t startv = (D1 && valid) ? starts[first + t] : 0u;
+    const uint64_t in_base = reinterpret_cast<uint64_t>(in);
+    const __amdgpu_buffer_rsrc_t ors = make_rsrc(out + first * n, nr * n * 4u);
+    uint32_t usedv = 0u; // lane j: bytes block j consumed
+    uint32_t js = 0;
+    while (js < nr)
+    {
+        const uint64_t cb = (in_base + readlane_u64(o, js)) & ~15ull; // window base (16-aligned)
+        const uint64_t lim = cb - in_base + kHWin;                     // stream offset past the window
+        // the window: blocks js.. up to the first one that is implausible or ends past lim
+        const uint64_t stop = __ballot(t >= js && (!valid || len == 0xFFFFFFFFu || e > lim));
+        const uint32_t je = stop ? static_cast<uint32_t>(__builtin_ctzll(stop)) : 64u;
+        if (je == js)
+        {
+            ++js; // implausible block: left undecoded, reported by the length check
+            continue;
+        }
+        const uint32_t span = static_cast<uint32_t>(in_base + readlane_u64(e, je - 1u) - cb);
+        const uint32_t avail = static_cast<uint32_t>(min_u64(in_base + in_bytes - cb, kHWin));
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(cb), avail);
+        for (uint32_t x = 16u * t; x < span; x += 1024u)
+            reinterpret_cast<u32x4 *>(slot)[x >> 4] = load16_guarded(reinterpret_cast<const uint8_t *>(cb), rs, x, avail);
+        wave_lds_sync();
+        // lane j in [js, je): parse block j's header
+        const bool inw = t >= js && t < je;
+        const uint32_t s = inw ? static_cast<uint32_t>(in_base + o - cb) : 0u;
+        const uint32_t hw = lds_u32(slot, s);
+        const uint32_t h = hw & 0xFFu;
+        uint32_t pk, cval = 0u, used = 0u;
+        if ((h & 0xC0u) == 0xC0u)
+        {
+            const uint32_t b = h & 0x3Fu;
+            cval = lds_u32(slot, s + 1u) & mask32(b);
+            used = 1u + ((b + 7u) >> 3);
+            pk = (kH32Const << 18);
+        }
+        else if (h & 0x40u)
+            pk = s | (kH32Vbyte << 18);
+        else
+        {
+            const uint32_t b = min(h & 0x7Fu, 32u);
+            const uint32_t bx = (h & 0x80u) ? min((hw >> 8) & 0xFFu, 32u) : 0u;
+            uint32_t P = s + ((h & 0x80u) ? 2u : 1u), kind = kH32Plain;
+            if (bx != 0u)
+            {
+                uint64_t bm[4];
+                uint32_t pc[4];
+                h32_bitmap(slot, s + 2u, n, bm, pc);
+                const uint32_t xn = (pc[0] + pc[1]) + (pc[2] + pc[3]);
+                P = s + 2u + pad8d(n) + pad8d(xn * bx);
+                kind = kH32Bitmap;
+            }
+            used = (P - s) + pad8d(n * b);
+            pk = P | (b << 12) | (kind << 18) | (bx << 20);
+        }
+        usedv = inw ? used : usedv;
+        for (uint32_t jj = js; jj < je; ++jj)
+        {
+            const uint32_t w = rl(pk, jj);
+            const uint32_t kind = (w >> 18) & 3u;
+            uint32_t v[4] = {0u, 0u, 0u, 0u};
+            if (kind == kH32Vbyte)
+            {
+                uint32_t cm;
+                const uint32_t u = decode_block_g<Fmt::H32>(slot, w & 0xFFFu, n, scratch[wv], t, v, &cm);
+                usedv = t == jj ? u : usedv;
+            }
+            else if (kind == kH32Const)
+            {
+                const uint32_t c = rl(cval, jj);
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j)
+                    v[j] = c;
+            }
+            else
+            {
+                const uint32_t P = w & 0xFFFu, b = (w >> 12) & 63u;
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j)
+                {
+                    const uint32_t el = t + 64u * j;
+                    if (64u * j < n)
+                        v[j] = (el < n && b) ? lds_bits(slot, P * 8u + el * b, b) : 0u;
+                }
+                if (kind == kH32Bitmap)
+                {
+                    // exceptions: bx-bit values after the bitmap, in element order
+                    // (p4dec32.cpp:96-120); rank of element t + 64j from the bitmap
+                    const uint32_t bx = (w >> 20) & 63u;
+                    const uint32_t sb = uni(static_cast<uint32_t>(in_base + readlane_u64(o, jj) - cb));
+                    uint64_t bm[4];
+                    uint32_t pc[4];
+                    h32_bitmap(slot, sb + 2u, n, bm, pc);
+                    const uint32_t xs = sb + 2u + pad8d(n);
+                    uint32_t before = 0;
+#pragma unroll
+                    for (uint32_t j = 0; j < 4; ++j)
+                    {
+                        if ((bm[j] >> t) & 1ull)
+                        {
+                            const uint32_t k = before + static_cast<uint32_t>(__builtin_popcountll(bm[j] & lanemask_lt()));
+                            v[j] |= shl32(lds_bits(slot, xs * 8u + k * bx, bx), b);
+                        }
+                        before += pc[j];
+                    }
+                }
+            }
+            if constexpr (D1)
+                (void)delta1_g<uint32_t>(v, n, rl(startv, jj), t);
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+            {
+                const uint32_t el = t + 64u * j;
+                if (64u * j < n)
+                    __builtin_amdgcn_raw_buffer_store_b32(v[j], ors, static_cast<int>(el < n ? (jj * n + el) * 4u : 0x80000000u), 0, TPF_H32_STORE_AUX);
+            }
+        }
+        wave_lds_sync(); // the next window overwrites the slot
+        js = je;
+    }
+    const uint64_t bad = __ballot(valid && usedv != len);
+    if (err != nullptr && t == 0 && bad != 0u)
+        atomicMin(err, static_cast<unsigned long long>(first + __builtin_ctzll(bad)));
+}
+
 // ---- run-pipelined encode for the one-block units ------------------------
 // Plan -> scan -> write as the 256v32 encoder; every wave owns a
 // contiguous run of kGRun units whose values arrive through one buffer
@@ -325,6 +519,18 @@ hipError_t dec_fmt(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, 
     return hipGetLastError();
 }
 
+hipError_t dec_h32w(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t n, uint32_t * out,
+                    const uint32_t * starts, unsigned long long * err, hipStream_t s)
+{
+    const uint64_t per_wg = 4ull * dev::kHRun;
+    const uint32_t g = static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg);
+    if (starts)
+        hipLaunchKernelGGL((dev::k_dec_h32w<true>), dim3(g), dim3(256), 0, s, in, in_bytes, off, nblocks, n, out, starts, err);
+    else
+        hipLaunchKernelGGL((dev::k_dec_h32w<false>), dim3(g), dim3(256), 0, s, in, in_bytes, off, nblocks, n, out, starts, err);
+    return hipGetLastError();
+}
+
 template <dev::Fmt F, bool D1>
 hipError_t enc_fmt_d(const void * in, uint64_t nblocks, uint32_t n, const void * starts, uint64_t start0, uint8_t * out,
                      uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t s)
@@ -371,6 +577,8 @@ hipError_t launch_dec_generic(int fmt, const uint8_t * in, uint64_t in_bytes, co
     switch (fmt)
     {
         case FMT_32:
+            if (n >= 1u && n <= 256u)
+                return dec_h32w(in, in_bytes, off, nblocks, n, static_cast<uint32_t *>(out), static_cast<const uint32_t *>(starts), err, s);
             return dec_fmt<dev::Fmt::H32>(in, in_bytes, off, nblocks, n, out, starts, err, s);
         case FMT_128V32:
             return dec_fmt<dev::Fmt::V128>(in, in_bytes, off, nblocks, n, out, starts, err, s);
