@@ -168,7 +168,7 @@ __device__ __forceinline__ void h32_bitmap(const uint32_t * slot, uint32_t s, ui
 }
 
 template <bool D1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void k_dec_h32w(const uint8_t * __restrict in, uint64_t in_bytes, const uint64_t * __restrict off,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8))) void k_dec_h32w(const uint8_t * __restrict in, uint64_t in_bytes, const uint64_t * __restrict off,
                                                    uint64_t nblocks, uint32_t n, uint32_t * __restrict out,
                                                    const uint32_t * __restrict starts, unsigned long long * __restrict err)
 {
@@ -190,25 +190,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void k_de
     const uint64_t in_base = reinterpret_cast<uint64_t>(in);
     const __amdgpu_buffer_rsrc_t ors = make_rsrc(out + first * n, nr * n * 4u);
     uint32_t usedv = 0u; // lane j: bytes block j consumed
-    uint32_t js = 0;
-    while (js < nr)
-    {
-        const uint64_t cb = (in_base + readlane_u64(o, js)) & ~15ull; // window base (16-aligned)
-        const uint64_t lim = cb - in_base + kHWin;                     // stream offset past the window
-        // the window: blocks js.. up to the first one that is implausible or ends past lim
-        const uint64_t stop = __ballot(t >= js && (!valid || len == 0xFFFFFFFFu || e > lim));
-        const uint32_t je = stop ? static_cast<uint32_t>(__builtin_ctzll(stop)) : 64u;
-        if (je == js)
+    // The window from the first plausible block at or after js: blocks
+    // js.. up to the first one that is implausible or ends past kHWin bytes
+    // from the window base (implausible blocks are skipped, left undecoded
+    // and reported by the length check).
+    auto find = [&](uint32_t & js, uint32_t & je, uint64_t & cb) {
+        for (; js < nr; ++js)
         {
-            ++js; // implausible block: left undecoded, reported by the length check
-            continue;
+            cb = (in_base + readlane_u64(o, js)) & ~15ull;
+            const uint64_t lim = cb - in_base + kHWin; // stream offset past the window
+            const uint64_t stop = __ballot(t >= js && (!valid || len == 0xFFFFFFFFu || e > lim));
+            je = stop ? static_cast<uint32_t>(__builtin_ctzll(stop)) : 64u;
+            if (je != js)
+                return;
         }
-        const uint32_t span = static_cast<uint32_t>(in_base + readlane_u64(e, je - 1u) - cb);
+    };
+    // the window's bytes into registers (lane t: bytes 16t + 1024k)
+    u32x4 R[3];
+    uint32_t span = 0u;
+    auto issue = [&](uint32_t je, uint64_t cb) {
+        span = static_cast<uint32_t>(in_base + readlane_u64(e, je - 1u) - cb);
         const uint32_t avail = static_cast<uint32_t>(min_u64(in_base + in_bytes - cb, kHWin));
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const void *>(cb), avail);
-        for (uint32_t x = 16u * t; x < span; x += 1024u)
-            reinterpret_cast<u32x4 *>(slot)[x >> 4] = load16_guarded(reinterpret_cast<const uint8_t *>(cb), rs, x, avail);
+#pragma unroll
+        for (uint32_t k = 0; k < 3; ++k)
+        {
+            const uint32_t x = 16u * t + 1024u * k;
+            if (x < span && x + 16u > avail)
+                R[k] = load16_guarded(reinterpret_cast<const uint8_t *>(cb), rs, x, avail); // straddles the stream end
+            else
+                R[k] = buf_load16(rs, x < span ? x : 0x80000000u);
+        }
+    };
+    uint32_t js = 0, je = 0;
+    uint64_t cb = 0;
+    find(js, je, cb);
+    if (js < nr)
+        issue(je, cb);
+    while (js < nr)
+    {
+#pragma unroll
+        for (uint32_t k = 0; k < 3; ++k)
+            if (16u * t + 1024u * k < span)
+                reinterpret_cast<u32x4 *>(slot)[t + 64u * k] = R[k];
         wave_lds_sync();
+        // the next window's loads fly while this one is decoded
+        uint32_t js2 = je, je2 = 0;
+        uint64_t cb2 = 0;
+        find(js2, je2, cb2);
+        if (js2 < nr)
+            issue(je2, cb2);
         // lane j in [js, je): parse block j's header
         const bool inw = t >= js && t < je;
         const uint32_t s = inw ? static_cast<uint32_t>(in_base + o - cb) : 0u;
@@ -304,7 +335,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void k_de
             }
         }
         wave_lds_sync(); // the next window overwrites the slot
-        js = je;
+        js = js2;
+        je = je2;
+        cb = cb2;
     }
     const uint64_t bad = __ballot(valid && usedv != len);
     if (err != nullptr && t == 0 && bad != 0u)
