@@ -46,6 +46,10 @@ constexpr uint32_t kEncRun = 16;  // blocks per wave run
 #ifndef TPF_ENC_NC_WRITE
 #define TPF_ENC_NC_WRITE 3
 #endif
+// cache policy of the plan pass's value loads (A/B knob: 2 = nt)
+#ifndef TPF_ENC_PLAN_AUX
+#define TPF_ENC_PLAN_AUX 0
+#endif
 // value chunks in flight per wave (NC: blocks j+1 .. j+NC-1 while j is encoded)
 constexpr uint32_t kEncNCPlan = TPF_ENC_NC_PLAN;
 constexpr uint32_t kEncNCWrite = TPF_ENC_NC_WRITE;
@@ -166,7 +170,7 @@ __device__ __forceinline__ void plan_run(const EncRun & R, const uint32_t * in, 
     const uint32_t stv = D1 ? R.start_lane(in, starts, start0, t) : 0u;
     szv = 0u;
     pwv = 0u;
-    R.template walk<kEncNCPlan, enc_load_aux(PROBE)>(t, [&](u32x4 v, uint32_t jj) {
+    R.template walk<kEncNCPlan, enc_load_aux(PROBE) | TPF_ENC_PLAN_AUX>(t, [&](u32x4 v, uint32_t jj) {
         if constexpr (D1)
             v = delta_encode(v, rl32(stv, jj), t);
         Plan32 P;

@@ -39,6 +39,17 @@ __device__ __forceinline__ uint32_t vblen32(uint32_t x)
     return x < 156u ? 1u : x < 16540u ? 2u : x < 2113692u ? 3u : x <= 0xFFFFFFu ? 4u : 5u;
 }
 
+#ifndef TPF_PLAN_FFBH
+#define TPF_PLAN_FFBH 1
+#endif
+// v_ffbh_u32(x) + 1: 0 for x == 0 (ffbh returns -1), else clz(x) + 1 = 33 - bw32(x)
+__device__ __forceinline__ uint32_t ffbh1(uint32_t x)
+{
+    uint32_t r;
+    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+    return r + 1u;
+}
+
 // hist: per-wave LDS scratch of kPlanHistU32 u32 (16-byte aligned).
 // 4 copies: the plan pass is bound by its LDS traffic as much as by conflicts
 // (A/B, C4 encode: 16 copies 447-451 G int32/s, 32 copies 337, 8 copies 454,
@@ -72,15 +83,27 @@ __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist
     }
     PlanHist::zero(hist, t);
     wave_lds_sync();
+#if TPF_PLAN_FFBH
+    // bins keyed by v_ffbh_u32(x) + 1: 0 for x == 0, else 33 - bw32(x) -- two
+    // VALU per value (ffbh, shift-add) instead of clz + zero select + address
+    PlanHist::add(hist, ffbh1(v.x), t);
+    PlanHist::add(hist, ffbh1(v.y), t);
+    PlanHist::add(hist, ffbh1(v.z), t);
+    PlanHist::add(hist, ffbh1(v.w), t);
+    wave_lds_sync();
+    const uint32_t cnt = PlanHist::get(hist, t == 0u ? 0u : (t <= 32u ? 33u - t : 64u)); // lane c: cnt[c] (0 for c > 32)
+#else
     PlanHist::add(hist, bw32(v.x), t);
     PlanHist::add(hist, bw32(v.y), t);
     PlanHist::add(hist, bw32(v.z), t);
     PlanHist::add(hist, bw32(v.w), t);
     wave_lds_sync();
     const uint32_t cnt = PlanHist::get(hist, t); // lane c holds cnt[c] (0 for c > 32)
+#endif
     wave_lds_sync();
     auto at = [&](uint32_t c) -> uint32_t {
-        uint32_t x = static_cast<uint32_t>(__shfl(static_cast<int>(cnt), static_cast<int>(c & 63u), 64));
+        // ds_bpermute takes lane c mod 64 from address bits [7:2]
+        const uint32_t x = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(c << 2), static_cast<int>(cnt)));
         return c < 64u ? x : 0u;
     };
     const uint32_t vbacc = at(t + 7u) + 2u * at(t + 15u) + 3u * at(t + 19u) + 4u * at(t + 25u);
@@ -116,7 +139,6 @@ __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist
         return P;
     }
     const uint32_t b = P.b;
-    const uint32_t m = mask32(b);
     if (kind == 0u)
     {
         // bitmap patch: xn = ec(b), already in lane b (no second reduction;
@@ -128,17 +150,22 @@ __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist
         P.raw = 0;
         return P;
     }
-    // vbyte: exception count (low half) and their vbyte bytes (high half,
-    // <= 5*256) in one reduction
-    const uint32_t cl = (v.x > m) + (v.y > m) + (v.z > m) + (v.w > m)
-                        + (((v.x > m ? vblen32(v.x >> b) : 0u) + (v.y > m ? vblen32(v.y >> b) : 0u)
-                            + (v.z > m ? vblen32(v.z >> b) : 0u) + (v.w > m ? vblen32(v.w >> b) : 0u))
-                           << 16);
-    const uint32_t tot = wave_sum(cl);
-    const uint32_t xn = tot & 0xFFFFu;
+    // vbyte: y = x >> b is non-zero exactly for the exceptions, and
+    // vblen32(y) = 1 + [y >= 156] + [y >= 16540] + [y >= 2113692] + [y >= 2^24],
+    // so the exception count and their vbyte bytes are ballot popcounts per
+    // threshold (compares on the VALU, counts on the scalar unit) instead of a
+    // per-value length under exec masks and a wave reduction
+    const uint32_t y0 = v.x >> b, y1 = v.y >> b, y2 = v.z >> b, y3 = v.w >> b; // b < maxb <= 32
+    auto count_ge = [&](uint32_t T) -> uint32_t {
+        return static_cast<uint32_t>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(y0 >= T))
+                                     + __builtin_popcountll(__builtin_amdgcn_ballot_w64(y1 >= T))
+                                     + __builtin_popcountll(__builtin_amdgcn_ballot_w64(y2 >= T))
+                                     + __builtin_popcountll(__builtin_amdgcn_ballot_w64(y3 >= T)));
+    };
+    const uint32_t xn = uni(count_ge(1u));
     P.xn = xn;
     P.bx = 33;
-    const uint32_t sumlen = tot >> 16;
+    const uint32_t sumlen = uni(xn + count_ge(156u) + count_ge(16540u) + count_ge(2113692u) + count_ge(0x1000000u));
     P.raw = (sumlen + 32u > 4u * xn) ? 1u : 0u;
     const uint32_t vsize = P.raw ? 1u + 4u * xn : sumlen;
     P.size = 2u + 32u * b + vsize + xn;
@@ -394,6 +421,10 @@ __device__ __forceinline__ void zero_image(uint32_t * img, uint32_t n16, uint32_
         reinterpret_cast<u32x4 *>(img)[i] = u32x4{0u, 0u, 0u, 0u};
 }
 
+// interior 16-byte chunks with non-temporal stores (A/B knob)
+#ifndef TPF_ENC_STORE_NT
+#define TPF_ENC_STORE_NT 0
+#endif
 __device__ __forceinline__ void copy_out_image16(const uint32_t * img, uint32_t sb, uint64_t dst, uint32_t size, uint64_t cap_end,
                                                  uint32_t t)
 {
@@ -417,9 +448,13 @@ __device__ __forceinline__ void copy_out_image16(const uint32_t * img, uint32_t 
         {
             const uint32_t q = (base >> 2) + 4u * k;
             const uint32_t w0 = img[q], w1 = img[q + 1], w2 = img[q + 2], w3 = img[q + 3], w4 = img[q + 4];
-            *(gu32x4 *)(a16 + 16u * k) =
-                u32x4{__builtin_amdgcn_alignbyte(w1, w0, bs), __builtin_amdgcn_alignbyte(w2, w1, bs),
-                      __builtin_amdgcn_alignbyte(w3, w2, bs), __builtin_amdgcn_alignbyte(w4, w3, bs)};
+            const u32x4 c = u32x4{__builtin_amdgcn_alignbyte(w1, w0, bs), __builtin_amdgcn_alignbyte(w2, w1, bs),
+                                  __builtin_amdgcn_alignbyte(w3, w2, bs), __builtin_amdgcn_alignbyte(w4, w3, bs)};
+#if TPF_ENC_STORE_NT
+            __builtin_nontemporal_store(c, (gu32x4 *)(a16 + 16u * k));
+#else
+            *(gu32x4 *)(a16 + 16u * k) = c;
+#endif
         }
         const uint32_t last = (end - 1u) >> 4; // chunk holding the block's last byte
         const uint32_t k = t < 16u ? 0u : last;

@@ -438,16 +438,32 @@ __device__ __forceinline__ PlanG plan_block_g(const typename FmtTraits<F>::T v[4
     }
     PlanGHist::zero(hist, t);
     wave_lds_sync();
+    uint32_t cnt, cnt64;
+    if constexpr (!wide)
+    {
+        // 32-bit values: bins keyed by v_ffbh_u32 + 1 (= 33 - bw, 0 for 0), as plan_block256
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j)
-        if (t + 64u * j < n)
-            PlanGHist::add(hist, bw64d(v[j]), t);
-    wave_lds_sync();
-    const uint32_t cnt = PlanGHist::get(hist, t);
-    const uint32_t cnt64 = uni(PlanGHist::get(hist, 64));
+        for (uint32_t j = 0; j < 4; ++j)
+            if (64u * j < n)
+                PlanGHist::add(hist, t + 64u * j < n ? ffbh1(static_cast<uint32_t>(v[j])) : 67u, t);
+        wave_lds_sync();
+        cnt = PlanGHist::get(hist, t == 0u ? 0u : (t <= 32u ? 33u - t : 68u));
+        cnt64 = 0u;
+    }
+    else
+    {
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+            if (t + 64u * j < n)
+                PlanGHist::add(hist, bw64d(v[j]), t);
+        wave_lds_sync();
+        cnt = PlanGHist::get(hist, t);
+        cnt64 = uni(PlanGHist::get(hist, 64));
+    }
     wave_lds_sync();
     auto at = [&](uint32_t c) -> uint32_t {
-        const uint32_t x = static_cast<uint32_t>(__shfl(static_cast<int>(cnt), static_cast<int>(c & 63u), 64));
+        // ds_bpermute takes lane c mod 64 from address bits [7:2]
+        const uint32_t x = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(c << 2), static_cast<int>(cnt)));
         return c < 64u ? x : (c == 64u ? cnt64 : 0u);
     };
     const uint32_t vbacc = at(t + 7u) + 2u * at(t + 15u) + 3u * at(t + 19u) + 4u * at(t + 25u);
@@ -490,21 +506,43 @@ __device__ __forceinline__ PlanG plan_block_g(const typename FmtTraits<F>::T v[4
         P.size = 2u + bmp + pad8d(xn * P.bx) + base_bytes<F>(NE, b);
         return P;
     }
-    const uint64_t m = mask64d(b);
-    uint32_t xc = 0, sl = 0;
+    uint32_t xn, sumlen;
+    if constexpr (!wide)
+    {
+        // exception count and vbyte bytes by ballot popcounts per vblen32
+        // threshold of y = x >> b (see plan_block256); b < maxb <= 32
+        uint32_t y[4];
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j)
-        if (t + 64u * j < n && static_cast<uint64_t>(v[j]) > m)
-        {
-            ++xc;
-            const uint64_t ex = static_cast<uint64_t>(v[j]) >> b;
-            sl += wide ? vblen64(ex) : vblen32(static_cast<uint32_t>(ex));
-        }
-    const uint32_t xs_tot = wave_sum(xc | (sl << 16)); // count | vbyte bytes (<= 9*256)
-    const uint32_t xn = xs_tot & 0xFFFFu;
+        for (uint32_t j = 0; j < 4; ++j)
+            y[j] = t + 64u * j < n ? static_cast<uint32_t>(v[j]) >> b : 0u;
+        auto count_ge = [&](uint32_t T) -> uint32_t {
+            uint32_t c = 0u;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+                if (64u * j < n)
+                    c += static_cast<uint32_t>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(y[j] >= T)));
+            return c;
+        };
+        xn = uni(count_ge(1u));
+        sumlen = uni(xn + count_ge(156u) + count_ge(16540u) + count_ge(2113692u) + count_ge(0x1000000u));
+    }
+    else
+    {
+        const uint64_t m = mask64d(b);
+        uint32_t xc = 0, sl = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+            if (t + 64u * j < n && static_cast<uint64_t>(v[j]) > m)
+            {
+                ++xc;
+                sl += vblen64(static_cast<uint64_t>(v[j]) >> b);
+            }
+        const uint32_t xs_tot = wave_sum(xc | (sl << 16)); // count | vbyte bytes (<= 9*256)
+        xn = xs_tot & 0xFFFFu;
+        sumlen = xs_tot >> 16;
+    }
     P.xn = xn;
     P.bx = W + 1u;
-    const uint32_t sumlen = xs_tot >> 16;
     constexpr uint32_t ES = W / 8u;
     P.raw = (sumlen + 32u > ES * xn) ? 1u : 0u;
     P.size = 2u + base_bytes<F>(NE, b) + (P.raw ? 1u + ES * xn : sumlen) + xn;

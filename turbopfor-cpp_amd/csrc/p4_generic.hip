@@ -167,7 +167,9 @@ __device__ __forceinline__ void h32_bitmap(const uint32_t * slot, uint32_t s, ui
     }
 }
 
-template <bool D1>
+// EPL: elements per lane (n <= 64 EPL), a template so the element loops
+// carry no per-block trip checks
+template <bool D1, uint32_t EPL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8))) void k_dec_h32w(const uint8_t * __restrict in, uint64_t in_bytes, const uint64_t * __restrict off,
                                                    uint64_t nblocks, uint32_t n, uint32_t * __restrict out,
                                                    const uint32_t * __restrict starts, unsigned long long * __restrict err)
@@ -298,7 +300,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
                 for (uint32_t j = 0; j < 4; ++j)
                 {
                     const uint32_t el = t + 64u * j;
-                    if (64u * j < n)
+                    if (j < EPL)
                         v[j] = (el < n && b) ? lds_bits(slot, P * 8u + el * b, b) : 0u;
                 }
                 if (kind == kH32Bitmap)
@@ -330,7 +332,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
             for (uint32_t j = 0; j < 4; ++j)
             {
                 const uint32_t el = t + 64u * j;
-                if (64u * j < n)
+                if (j < EPL)
                     __builtin_amdgcn_raw_buffer_store_b32(v[j], ors, static_cast<int>(el < n ? (jj * n + el) * 4u : 0x80000000u), 0, TPF_H32_STORE_AUX);
             }
         }
@@ -415,23 +417,24 @@ template <Fmt F, bool D1, bool WRITE, uint32_t NC = 3>
 __global__ __launch_bounds__(256) void k_enc_gr(const typename FmtTraits<F>::T * __restrict in, uint64_t nblocks, uint32_t n,
                                                  const typename FmtTraits<F>::T * __restrict starts,
                                                  typename FmtTraits<F>::T start0, uint64_t * __restrict off,
-                                                 uint32_t * __restrict run_tot, const uint64_t * __restrict run_pre,
+                                                 uint32_t * __restrict plan, uint32_t * __restrict run_tot, const uint64_t * __restrict run_pre,
                                                  const uint64_t * __restrict run_tile, uint8_t * __restrict out, uint64_t out_cap)
 {
     using G = UnitGeom<F, false>;
     using T = typename FmtTraits<F>::T;
     __shared__ uint32_t imgs[WRITE ? 4 : 1][WRITE ? (G::kSlot / 4 + 8) : 1];
-    __shared__ __attribute__((aligned(16))) uint32_t hist[4][kPlanGHistU32];
+    __shared__ __attribute__((aligned(16))) uint32_t hist[WRITE ? 1 : 4][WRITE ? 4 : kPlanGHistU32]; // plan pass only
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
     EncRunG<F> R;
     if (!R.init(in, nblocks, wv, n))
         return;
     const T stv = D1 ? R.start_lane(in, starts, start0, t) : T(0);
-    uint32_t szv = 0u;
+    uint32_t szv = 0u, pwv = 0u; // lane j: size and plan word of unit first+j
     uint32_t olo = 0u, ohi = 0u;
     if constexpr (WRITE)
     {
+        pwv = t < R.nr ? plan[R.first + t] : 0u;
         uint64_t ov, ev;
         run_offsets(off, R.first, R.nr, run_base(run_pre, run_tile, R.first / kGRun), t, ov, ev);
         szv = static_cast<uint32_t>(ev - ov);
@@ -451,14 +454,18 @@ __global__ __launch_bounds__(256) void k_enc_gr(const typename FmtTraits<F>::T *
                 st = static_cast<T>(__builtin_amdgcn_readlane(static_cast<int>(stv), static_cast<int>(jj)));
             delta_enc_g<T>(U.v, st, n, t);
         }
-        const PlanG P = plan_block_g<F>(U.v, n, hist[wv], t);
         if constexpr (!WRITE)
         {
+            const PlanG P = plan_block_g<F>(U.v, n, hist[wv], t);
             szv = t == jj ? P.size : szv;
+            pwv = t == jj ? (P.b | (P.bx << 8) | (P.xn << 16) | (P.raw << 25)) : pwv;
         }
         else
         {
+            // the plan pass's choice (b <= 64, bx <= 66, xn <= 256): not re-planned
             const uint32_t size = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(szv), static_cast<int>(jj)));
+            const uint32_t pw = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(pwv), static_cast<int>(jj)));
+            const PlanG P{pw & 0xFFu, (pw >> 8) & 0xFFu, size, (pw >> 16) & 0x1FFu, (pw >> 25) & 1u};
             const uint64_t o = (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ohi), static_cast<int>(jj)))) << 32)
                              | static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(olo), static_cast<int>(jj)));
             const uint64_t dst = out_base + o;
@@ -523,7 +530,10 @@ __global__ __launch_bounds__(256) void k_enc_gr(const typename FmtTraits<F>::T *
     if constexpr (!WRITE)
     {
         if (t < R.nr)
+        {
             off[R.first + t] = szv;
+            plan[R.first + t] = pwv;
+        }
         publish_run_total(run_tot, R.first / kGRun, t < R.nr ? szv : 0u, t);
     }
 }
@@ -535,6 +545,8 @@ namespace tpf
 
 namespace
 {
+
+size_t plan_bytes(uint64_t nblocks) { return (nblocks * 4u + 255u) & ~size_t(255); }
 
 template <dev::Fmt F>
 hipError_t dec_fmt(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t n, void * out,
@@ -557,10 +569,19 @@ hipError_t dec_h32w(const uint8_t * in, uint64_t in_bytes, const uint64_t * off,
 {
     const uint64_t per_wg = 4ull * dev::kHRun;
     const uint32_t g = static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg);
+    auto go = [&](auto d1, auto epl) {
+        hipLaunchKernelGGL((dev::k_dec_h32w<decltype(d1)::value, decltype(epl)::value>), dim3(g), dim3(256), 0, s, in, in_bytes, off, nblocks,
+                           n, out, starts, err);
+    };
+    using T1 = std::true_type;
+    using F1 = std::false_type;
+    using E1 = std::integral_constant<uint32_t, 1>;
+    using E2 = std::integral_constant<uint32_t, 2>;
+    using E4 = std::integral_constant<uint32_t, 4>;
     if (starts)
-        hipLaunchKernelGGL((dev::k_dec_h32w<true>), dim3(g), dim3(256), 0, s, in, in_bytes, off, nblocks, n, out, starts, err);
+        n <= 64u ? go(T1{}, E1{}) : n <= 128u ? go(T1{}, E2{}) : go(T1{}, E4{});
     else
-        hipLaunchKernelGGL((dev::k_dec_h32w<false>), dim3(g), dim3(256), 0, s, in, in_bytes, off, nblocks, n, out, starts, err);
+        n <= 64u ? go(F1{}, E1{}) : n <= 128u ? go(F1{}, E2{}) : go(F1{}, E4{});
     return hipGetLastError();
 }
 
@@ -574,19 +595,20 @@ hipError_t enc_fmt_d(const void * in, uint64_t nblocks, uint32_t n, const void *
     const uint64_t per_wg = 4ull * dev::kGRun;
     const uint32_t g = static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg);
     const uint64_t nruns = (nblocks + dev::kGRun - 1u) / dev::kGRun;
-    if (ws_bytes < RunScanWs<uint64_t>::bytes(nruns))
+    if (ws_bytes < generic_workspace(nblocks))
         return hipErrorInvalidValue;
-    const RunScanWs<uint64_t> rs = RunScanWs<uint64_t>::carve(ws, nruns);
-    hipLaunchKernelGGL((dev::k_enc_gr<F, D1, false>), dim3(g), dim3(256), 0, s, ip, nblocks, n, sp, static_cast<T>(start0), off, rs.tot,
-                       nullptr, nullptr, out, out_cap);
+    uint32_t * plan = static_cast<uint32_t *>(ws);
+    const RunScanWs<uint64_t> rs = RunScanWs<uint64_t>::carve(static_cast<uint8_t *>(ws) + plan_bytes(nblocks), nruns);
+    hipLaunchKernelGGL((dev::k_enc_gr<F, D1, false>), dim3(g), dim3(256), 0, s, ip, nblocks, n, sp, static_cast<T>(start0), off, plan,
+                       rs.tot, nullptr, nullptr, out, out_cap);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return e;
     e = launch_run_scan_u64(rs.tot, nruns, rs.pre, rs.tile, off + nblocks, s);
     if (e != hipSuccess)
         return e;
-    hipLaunchKernelGGL((dev::k_enc_gr<F, D1, true>), dim3(g), dim3(256), 0, s, ip, nblocks, n, sp, static_cast<T>(start0), off, nullptr,
-                       rs.pre, rs.tile, out, out_cap);
+    hipLaunchKernelGGL((dev::k_enc_gr<F, D1, true>), dim3(g), dim3(256), 0, s, ip, nblocks, n, sp, static_cast<T>(start0), off, plan,
+                       nullptr, rs.pre, rs.tile, out, out_cap);
     return hipGetLastError();
 }
 
@@ -600,7 +622,8 @@ hipError_t enc_fmt(const void * in, uint64_t nblocks, uint32_t n, bool d1, const
 
 } // namespace
 
-size_t generic_workspace(uint64_t nblocks) { return RunScanWs<uint64_t>::bytes((nblocks + dev::kGRun - 1u) / dev::kGRun); }
+// plan words (one per unit, 256-B aligned) + the run scan
+size_t generic_workspace(uint64_t nblocks) { return plan_bytes(nblocks) + RunScanWs<uint64_t>::bytes((nblocks + dev::kGRun - 1u) / dev::kGRun); }
 
 hipError_t launch_dec_generic(int fmt, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t n,
                               void * out, const void * starts, unsigned long long * err, hipStream_t s)
