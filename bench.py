@@ -916,7 +916,7 @@ def run_c1(args, world, rank, dev, T):
     roof = {"bound": "hbm", "achieved": round(alg / (avg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), **traffic_fields("c1", nb),
             "kernel_ms_avg": round(avg_ms, 4),
-            "kernel": "tpf::dev::k_dec_gr<H32> (run-pipelined horizontal p4Dec32 batch)",
+            "kernel": "tpf::dev::k_dec_h32w (windowed horizontal p4Dec32 batch: 64-block wave runs, windows staged whole, lane-parsed headers)",
             "per_rank": per_rank}
     cpu = None
     if not args.no_cpu_baseline and world == 1:

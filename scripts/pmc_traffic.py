@@ -26,7 +26,7 @@ def _dec(mode):
 KERNELS = {
     "c2": ([_dec(0)], "tpf::dev::k_dec256v32w<StartMode::None>"),
     "c3": ([_dec(1)], "tpf::dev::k_dec256v32w<StartMode::PerBlock>"),
-    "c1": ([lambda n: "k_dec_gr" in n and ("FmtE0E" in n or "Fmt)0," in n)], "tpf::dev::k_dec_gr<Fmt::H32>"),
+    "c1": ([lambda n: "k_dec_h32w" in n], "tpf::dev::k_dec_h32w (windowed p4Dec32 batch)"),
     # chained list: phase A (block sums) + phase B (prefix decode); the run
     # scan between them (p4_scan.hip: 156K u32 run sums, ~1 MB) is not counted
     "c3chain": ([lambda n: "k_dsum256v32_lanes" in n, _dec(2)], "k_dsum256v32_lanes (phase A) + k_dec256v32w<Prefix>"),

@@ -57,15 +57,16 @@ def test_step_sums_its_kernels_and_merges(tmp_path):
 
 
 def test_round3_kernels(tmp_path):
-    """c3chain = lane-per-block phase A + prefix decode; c1 = the run-pipelined generic decoder;
+    """c3chain = lane-per-block phase A + prefix decode; c1 = the windowed p4Dec32 decoder;
     c4_64 = the 64-bit leg's three kernels (NB = 2, non-D1)."""
     out = tmp_path / "t.json"
     dsum = "void tpf::dev::k_dsum256v32_lanes<16384u>(tpf::dev::DecArgs)"
     dec2 = "void tpf::dev::k_dec256v32w<(tpf::dev::StartMode)2, 16u, 10u, 6u, 7, true>(tpf::dev::DecArgs)"
     d = _run(tmp_path, "c3chain", [(dsum, 10), (dec2, 20)], [(dsum, 0), (dec2, 30)], out)
     assert d["FETCH_SIZE_KiB_median"] == 30 and d["WRITE_SIZE_KiB_median"] == 30
-    pair = "void tpf::dev::k_dec_gr<(tpf::dev::Fmt)0, false>(unsigned char const*, unsigned long)"
-    d = _run(tmp_path, "c1", [(pair, 4)], [(pair, 9)], out)
+    win = "void tpf::dev::k_dec_h32w<false, 2u>(unsigned char const*, unsigned long)"
+    gen = "void tpf::dev::k_dec_gr<(tpf::dev::Fmt)0, false>(unsigned char const*, unsigned long)"
+    d = _run(tmp_path, "c1", [(win, 4), (gen, 50)], [(win, 9), (gen, 50)], out)
     assert d["hbm_bytes_per_launch"] == (2 * 4 + 9) * 1024
     p64 = "void tpf::dev::k_enc128v64_plan<2u, false>(unsigned long const*, unsigned long)"
     w64 = "void tpf::dev::k_enc128v64_write<2u, false>(unsigned long const*, unsigned long)"

@@ -411,19 +411,35 @@ __device__ __forceinline__ PlanG plan_block_g(const typename FmtTraits<F>::T v[4
     constexpr bool wide = Tr::wide;
     const uint32_t NE = Tr::N ? Tr::N : n;
     PlanG P{0, 0, 1, 0, 0};
-    uint64_t o = 0;
+    uint32_t maxb;
+    uint64_t first;
+    if constexpr (wide)
+    {
+        uint64_t o = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j)
-        if (t + 64u * j < n)
-            o |= v[j];
-    const uint64_t orv = wave_or64(o);
-    if (orv == 0)
+        for (uint32_t j = 0; j < 4; ++j)
+            if (t + 64u * j < n)
+                o |= v[j];
+        const uint64_t orv = wave_or64(o);
+        maxb = bw64d(orv);
+        first = readlane64(static_cast<uint64_t>(v[0]), 0);
+    }
+    else
+    {
+        // 32-bit values: one wave OR and one readlane
+        uint32_t o = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+            if (t + 64u * j < n)
+                o |= static_cast<uint32_t>(v[j]);
+        maxb = bw32(uni(wave_or(o)));
+        first = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(v[0])), 0));
+    }
+    if (maxb == 0u)
     {
         P.size = 1u + base_bytes<F>(NE, 0);
         return P;
     }
-    const uint32_t maxb = bw64d(orv);
-    const uint64_t first = readlane64(static_cast<uint64_t>(v[0]), 0);
     // constant block: a ballot, not a wave reduction
     bool same = true;
 #pragma unroll

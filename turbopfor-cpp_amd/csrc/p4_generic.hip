@@ -347,6 +347,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
 }
 
 // ---- run-pipelined encode for the one-block units ------------------------
+// A/B knob: 1 = copy a unit out with 16-byte stores and byte-store edges
+// (copy_out_image16) instead of the dword loop.  C1 encode, one box: 314 vs
+// 342 G int32/s for the dword loop -- kept at 0.
+#ifndef TPF_GENC_COPY16
+#define TPF_GENC_COPY16 0
+#endif
 // Plan -> scan -> write as the 256v32 encoder; every wave owns a
 // contiguous run of kGRun units whose values arrive through one buffer
 // descriptor with the next NC-1 units in flight (the first version, one unit
@@ -422,7 +428,7 @@ __global__ __launch_bounds__(256) void k_enc_gr(const typename FmtTraits<F>::T *
 {
     using G = UnitGeom<F, false>;
     using T = typename FmtTraits<F>::T;
-    __shared__ uint32_t imgs[WRITE ? 4 : 1][WRITE ? (G::kSlot / 4 + 8) : 1];
+    __shared__ __attribute__((aligned(16))) uint32_t imgs[WRITE ? 4 : 1][WRITE ? (G::kSlot / 4 + 8) : 1];
     __shared__ __attribute__((aligned(16))) uint32_t hist[WRITE ? 1 : 4][WRITE ? 4 : kPlanGHistU32]; // plan pass only
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
@@ -469,6 +475,18 @@ __global__ __launch_bounds__(256) void k_enc_gr(const typename FmtTraits<F>::T *
             const uint64_t o = (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ohi), static_cast<int>(jj)))) << 32)
                              | static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(olo), static_cast<int>(jj)));
             const uint64_t dst = out_base + o;
+#if TPF_GENC_COPY16
+            // the block at image byte 16 + (dst & 15): copy_out_image16 (p4_enc32.h)
+            // writes whole 16-byte chunks and the two edge chunks byte by byte
+            // (the dword loop it replaced took a byte loop on its edge lanes)
+            const uint32_t s0 = 16u + static_cast<uint32_t>(dst & 15u);
+            emit_block_g<F>(img, s0, P, U.v, n, t);
+            wave_lds_sync();
+            copy_out_image16(img, s0, dst, size, cap_end, t);
+            wave_lds_sync();
+            zero_image(img, (s0 + size + 15u) >> 4, t);
+            wave_lds_sync();
+#else
             const uint32_t phase = static_cast<uint32_t>(dst & 3u);
             emit_block_g<F>(img, phase, P, U.v, n, t);
             wave_lds_sync();
@@ -499,6 +517,7 @@ __global__ __launch_bounds__(256) void k_enc_gr(const typename FmtTraits<F>::T *
             for (uint32_t d = t; d < nd; d += 64u)
                 img[d] = 0u;
             wave_lds_sync();
+#endif
         }
     };
     if constexpr (WRITE)
