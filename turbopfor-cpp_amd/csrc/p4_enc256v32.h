@@ -189,6 +189,20 @@ __device__ __forceinline__ void plan_run(const EncRun & R, const uint32_t * in, 
     });
 }
 
+// copy-out of a built block (A/B knob): 0 = 16-byte chunks with byte-store
+// edges (copy_out_image16), 1 = dword stores (copy_out_dw)
+#ifndef TPF_ENC_COPY_DW
+#define TPF_ENC_COPY_DW 0
+#endif
+__device__ __forceinline__ void copy_out(const uint32_t * img, uint32_t sb, uint64_t dst, uint32_t size, uint64_t cap_end, uint32_t t)
+{
+#if TPF_ENC_COPY_DW
+    copy_out_dw(img, sb, dst, size, cap_end, t);
+#else
+    copy_out_image16(img, sb, dst, size, cap_end, t);
+#endif
+}
+
 // Write a run: lane j of (szv, pwv, olo/ohi) = size, plan word and byte
 // offset of block R.first+j.  img: the wave's zeroed LDS image (left zeroed).
 template <bool D1, int PROBE = 0>
@@ -207,7 +221,7 @@ __device__ __forceinline__ void write_run(const EncRun & R, const uint32_t * in,
         {
             reinterpret_cast<u32x4 *>(img)[4 + t] = v;
             wave_lds_sync();
-            copy_out_image16(img, kImgLead, dst, size, cap_end, t);
+            copy_out(img, kImgLead, dst, size, cap_end, t);
             wave_lds_sync();
             zero_image(img, kImgU32 / 4u, t);
             wave_lds_sync();
@@ -215,7 +229,7 @@ __device__ __forceinline__ void write_run(const EncRun & R, const uint32_t * in,
         }
         const uint32_t sb = emit_block256<true>(img, val, P, v, t);
         wave_lds_sync();
-        copy_out_image16(img, sb, dst, size, cap_end, t);
+        copy_out(img, sb, dst, size, cap_end, t);
         wave_lds_sync();
         // only [0, sb + size) can be non-zero: clear it for the next block
         zero_image(img, min((sb + size + 15u) >> 4, kImgU32 / 4u), t);

@@ -471,4 +471,34 @@ __device__ __forceinline__ void copy_out_image16(const uint32_t * img, uint32_t 
     }
 }
 
+
+// Copy a block built in an LDS image (block byte 0 at image byte sb >= 4) to
+// dst with dword stores: destination dword d of a0 = dst & ~3 holds image
+// bytes base + 4d .. (base = sb - (dst & 3)), realigned by v_alignbyte; the
+// first and last dwords, shared with the neighbouring blocks, byte by byte.
+// (The C1 encoder measured this 9% faster than 16-byte chunks with byte-store
+// edges: an edge costs at most 3 byte stores per side instead of 15.)
+__device__ __forceinline__ void copy_out_dw(const uint32_t * img, uint32_t sb, uint64_t dst, uint32_t size, uint64_t cap_end, uint32_t t)
+{
+    typedef __attribute__((address_space(1))) uint32_t gu32;
+    typedef __attribute__((address_space(1))) uint8_t gu8;
+    const uint32_t ph = static_cast<uint32_t>(dst & 3u);
+    const uint32_t base = sb - ph, qb = base >> 2, bs = base & 3u;
+    const uint64_t a0 = dst & ~3ull;
+    const uint32_t end = ph + size;
+    const uint32_t nd = (end + 3u) >> 2;
+    for (uint32_t d = t; d < nd; d += 64u)
+    {
+        const uint32_t w = __builtin_amdgcn_alignbyte(img[qb + d + 1u], img[qb + d], bs);
+        const uint64_t ga = a0 + 4u * d;
+        const uint32_t lo = 4u * d;
+        if (lo >= ph && lo + 4u <= end && ga + 4u <= cap_end)
+            *(gu32 *)ga = w;
+        else
+            for (uint32_t x = 0; x < 4; ++x)
+                if (lo + x >= ph && lo + x < end && ga + x < cap_end)
+                    *(gu8 *)(ga + x) = static_cast<uint8_t>(w >> (8u * x));
+    }
+}
+
 } // namespace tpf::dev
