@@ -119,6 +119,10 @@ __device__ __forceinline__ uint64_t delta1_128v64(uint64_t & x0, uint64_t & x1, 
     return start + readlane_u64(incl, 63);
 }
 
+// output store policy (A/B knob): 0 = nt, 1 = sc1 nt through a run descriptor
+#ifndef TPF_D64_SC1NT
+#define TPF_D64_SC1NT 0
+#endif
 template <uint32_t NB, bool D1>
 __global__ __launch_bounds__(256, 4) void k_dec128v64w(const uint8_t * __restrict in, uint64_t in_bytes,
                                                        const uint64_t * __restrict off, uint64_t nunits,
@@ -147,6 +151,9 @@ __global__ __launch_bounds__(256, 4) void k_dec128v64w(const uint8_t * __restric
     const uint64_t startv = (D1 && valid) ? starts[unit] : 0ull;
     UsedLanes usedv;
     uint64_t * const out_run = out + first * (128u * NB);
+#if TPF_D64_SC1NT
+    const __amdgpu_buffer_rsrc_t ors = make_rsrc(out_run, n * NB * 1024u);
+#endif
 
     auto consume = [&](const Chunk & c, uint32_t jj) {
         const uint32_t ctl = P.stage(c, jj, slot, t);
@@ -160,8 +167,14 @@ __global__ __launch_bounds__(256, 4) void k_dec128v64w(const uint8_t * __restric
             s += decode_block128v64(slot, s, scr, t, x0, x1);
             if constexpr (D1)
                 carry = delta1_128v64(x0, x1, carry);
+#if TPF_D64_SC1NT
+            // "sc1 nt" through the run's descriptor (the hot path's policy for whole 1 KB lines)
+            st16_run(ors, (jj * NB + u) * 1024u + 16u * t,
+                     u32x4{static_cast<uint32_t>(x0), static_cast<uint32_t>(x0 >> 32), static_cast<uint32_t>(x1), static_cast<uint32_t>(x1 >> 32)});
+#else
             typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
             __builtin_nontemporal_store(u64x2{x0, x1}, reinterpret_cast<u64x2 *>(out_run + (jj * NB + u) * 128u) + t);
+#endif
             wave_lds_sync();
         }
         usedv.put(s - s0, jj, t);
