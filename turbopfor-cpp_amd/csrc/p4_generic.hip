@@ -300,8 +300,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
                 for (uint32_t j = 0; j < 4; ++j)
                 {
                     const uint32_t el = t + 64u * j;
+                    // no per-element condition (it made two exec-mask sections per
+                    // block): b = 0 reads mask 0, and values of elements past n go
+                    // nowhere (their stores take an out-of-range offset); their LDS
+                    // reads may run past this wave's window, which is harmless
                     if (j < EPL)
-                        v[j] = (el < n && b) ? lds_bits(slot, P * 8u + el * b, b) : 0u;
+                        v[j] = lds_bits(slot, P * 8u + el * b, b);
                 }
                 if (kind == kH32Bitmap)
                 {
