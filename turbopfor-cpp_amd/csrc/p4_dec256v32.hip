@@ -399,12 +399,16 @@ namespace
 // one 16-byte load per lane per block with six blocks in flight (ONE / NC 6),
 // 7 waves per SIMD.  (C2 899 -> 906, C3 1080 -> 1106 G int32/s vs two loads
 // per block with three in flight)
+// load / store cache policy of the decode (POL bits of ld16 / st16, p4_dec_run.h)
+#ifndef TPF_DEC_POL
+#define TPF_DEC_POL (2 | 8)
+#endif
 template <dev::StartMode SM>
 hipError_t launch_mode(const dev::DecArgs & A, hipStream_t stream)
 {
     constexpr uint64_t per_wg = 4ull * dev::kRunDefault;
     const uint32_t grid = static_cast<uint32_t>((A.nblocks + per_wg - 1) / per_wg);
-    hipLaunchKernelGGL((dev::k_dec256v32w<SM, dev::kRunDefault, 2 | 8, 6, 7, true>), dim3(grid), dim3(256), 0, stream, A);
+    hipLaunchKernelGGL((dev::k_dec256v32w<SM, dev::kRunDefault, TPF_DEC_POL, 6, 7, true>), dim3(grid), dim3(256), 0, stream, A);
     return hipGetLastError();
 }
 } // namespace
