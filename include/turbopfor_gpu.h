@@ -142,7 +142,11 @@ int tpf_probe_enc256v32(int mode, const uint32_t *d_in, uint64_t nblocks, uint8_
 #define TPF_FMT_128V64 4
 #define TPF_FMT_256V64 5
 
-/* tpf_enc_batch requires out_cap >= tpf_enc_bound(fmt, nblocks, n) (TPF_EINVAL otherwise). */
+/* tpf_enc_batch requires out_cap >= tpf_enc_bound(fmt, nblocks, n) (TPF_EINVAL otherwise).
+ * tpf_dec_batch reports through d_err (first such block index) any block whose
+ * parse disagrees with its offsets; for TPF_FMT_32 (the windowed decoder) also
+ * any block whose offsets span more than 2,544 bytes or run past in_bytes --
+ * a p4Enc32 block of n <= 256 values is at most about 1 KB. */
 uint64_t tpf_enc_bound(int fmt, uint64_t nblocks, unsigned n);
 size_t tpf_enc_workspace_size(int fmt, uint64_t nblocks, unsigned n);
 int tpf_dec_batch(int fmt, const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks, unsigned n,
