@@ -108,6 +108,14 @@ int tpf_host_dec(int fmt, const uint8_t *h_in, uint64_t in_bytes, const uint64_t
 int tpf_host_enc(int fmt, const void *h_vals, uint64_t nblocks, unsigned n, int d1, const void *h_starts, uint64_t start0,
                  uint8_t *h_out, uint64_t out_cap, uint64_t *h_off);
 void tpf_host_release(void);
+/* Decode one host stream on several GPUs at once: the blocks are cut into ndev
+ * contiguous shards of about equal bytes and shard d runs tpf_host_dec's
+ * pipeline on device devs[d] from its own thread (each GPU brings its own
+ * PCIe link).  Arguments and checks as tpf_host_dec; a failing shard's
+ * message names the shard (its block numbers are shard-relative).  devs may
+ * repeat a device (two pipelines on one GPU). */
+int tpf_host_dec_multi(const int *devs, int ndev, int fmt, const uint8_t *h_in, uint64_t in_bytes, const uint64_t *h_off,
+                       uint64_t nblocks, unsigned n, void *h_vals, const void *h_starts);
 
 #ifdef __cplusplus
 }

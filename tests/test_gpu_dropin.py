@@ -376,3 +376,45 @@ def test_per_block_calls_beside_host_stream_frees(monkeypatch):
     assert not th.is_alive()
     assert not errors, errors
     assert calls[0] > 0
+
+
+def test_host_dec_multi_vs_single():
+    """tpf_host_dec_multi (SURVEY.md 8 f3 across GPUs): the stream cut into
+    shards, one pipeline thread per listed device -- on a one-GPU box the same
+    device listed 1, 2 and 3 times -- matches tpf_host_dec and the oracle for
+    plain and delta-1 decodes (pageable numpy buffers, registered once for
+    all shards), and a corrupt block fails the call naming its shard."""
+    L = capi()
+    L.tpf_host_dec_multi.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                                     ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]
+    ndev = torch.cuda.device_count()
+    blocks = np.concatenate([datagen.c2_blocks(2000, bw, 10, seed=9) for bw in (2, 11, 23, 32)])
+    packed, off = oracle_lib.enc256v32_batch(blocks)
+    nb = len(blocks)
+    vals, starts = datagen.c3_postings(4001)
+    p1, o1 = oracle_lib.enc256v32_batch(vals, starts=starts)
+    for k in (1, 2, 3):
+        devs = np.array([i % ndev for i in range(k)], dtype=np.int32)
+        back = np.zeros_like(blocks)
+        rc = L.tpf_host_dec_multi(devs.ctypes.data, k, 2, packed.ctypes.data, len(packed), off.ctypes.data, nb, 256,
+                                  back.ctypes.data, None)
+        assert rc == 0, L.tpf_last_error()
+        np.testing.assert_array_equal(back, blocks)
+        back = np.zeros_like(blocks)  # offsets scanned from the headers
+        assert L.tpf_host_dec_multi(devs.ctypes.data, k, 2, packed.ctypes.data, len(packed), None, nb, 256,
+                                    back.ctypes.data, None) == 0, L.tpf_last_error()
+        np.testing.assert_array_equal(back, blocks)
+        back1 = np.zeros_like(vals)
+        assert L.tpf_host_dec_multi(devs.ctypes.data, k, 2, p1.ctypes.data, len(p1), o1.ctypes.data, 4001, 256,
+                                    back1.ctypes.data, starts.ctypes.data) == 0, L.tpf_last_error()
+        np.testing.assert_array_equal(back1, vals)
+    bad = off.astype(np.uint64).copy()
+    bad[7000] += 1  # block 6999 one byte too long: shard 1 of 2 (blocks 4000.. hold the wider widths' bytes)
+    devs = np.zeros(2, dtype=np.int32)
+    back = np.zeros_like(blocks)
+    rc = L.tpf_host_dec_multi(devs.ctypes.data, 2, 2, packed.ctypes.data, len(packed), bad.ctypes.data, nb, 256,
+                              back.ctypes.data, None)
+    assert rc == -4
+    assert b"shard" in L.tpf_last_error()
+    assert L.tpf_host_dec_multi(devs.ctypes.data, 0, 2, packed.ctypes.data, len(packed), off.ctypes.data, nb, 256,
+                                back.ctypes.data, None) == -1

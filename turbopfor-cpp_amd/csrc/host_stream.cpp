@@ -22,6 +22,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <optional>
+#include <thread>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -272,6 +274,9 @@ void need_device()
         throw Err(TPF_ENODEV, "no HIP device visible (turbopfor_amd has no CPU fallback)");
 }
 
+int host_dec_impl(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_t * h_off, uint64_t nblocks, unsigned n,
+                  void * h_vals, const void * h_starts, bool take_pause);
+
 } // namespace
 
 extern "C" {
@@ -283,6 +288,16 @@ extern "C" {
 int tpf_host_dec(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_t * h_off, uint64_t nblocks, unsigned n,
                  void * h_vals, const void * h_starts)
 {
+    return host_dec_impl(fmt, h_in, in_bytes, h_off, nblocks, n, h_vals, h_starts, true);
+}
+
+} // extern "C"
+
+namespace
+{
+int host_dec_impl(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_t * h_off, uint64_t nblocks, unsigned n,
+                  void * h_vals, const void * h_starts, bool take_pause)
+{
     try
     {
         if (nblocks == 0)
@@ -291,7 +306,10 @@ int tpf_host_dec(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_
         // the resident per-block server stays stopped (and per-block calls
         // wait) for the whole call: HIP's frees, host (un)registrations and
         // device-wide waits would otherwise wait on the server's stream
-        const tpf::PerblockPause pause;
+        // (tpf_host_dec_multi holds it once for all its shards)
+        std::optional<tpf::PerblockPause> pause;
+        if (take_pause)
+            pause.emplace();
         std::vector<uint64_t> scanned;
         if (!h_off)
         {
@@ -368,6 +386,122 @@ int tpf_host_dec(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_
             }
         if (bad != ~0ull)
             throw Err(TPF_ECORRUPT, "tpf_host_dec: block " + std::to_string(bad) + " parses to a length other than its offsets");
+        return TPF_OK;
+    }
+    catch (const Err & e)
+    {
+        return report(e, e.code);
+    }
+    catch (const std::exception & e)
+    {
+        return report(e, TPF_EHIP);
+    }
+}
+
+} // namespace
+
+extern "C" {
+
+// Multi-GPU decode of one host stream ("across streams and
+// GPUs"): the blocks are cut into ndev contiguous shards of about equal
+// bytes, and shard d runs tpf_host_dec's pipeline on device devs[d] from a
+// thread of its own (each device has its own PCIe link and copy engines).
+// The input and output ranges are registered once, portable, for all
+// devices; the per-block servers stay paused for the whole call.
+int tpf_host_dec_multi(const int * devs, int ndev, int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_t * h_off,
+                       uint64_t nblocks, unsigned n, void * h_vals, const void * h_starts)
+{
+    try
+    {
+        if (nblocks == 0)
+            return TPF_OK;
+        need_device();
+        int cnt = 0;
+        hc(hipGetDeviceCount(&cnt), "hipGetDeviceCount");
+        if (!devs || ndev < 1 || ndev > 64)
+            throw Err(TPF_EINVAL, "tpf_host_dec_multi: need 1..64 devices");
+        for (int d = 0; d < ndev; ++d)
+            if (devs[d] < 0 || devs[d] >= cnt)
+                throw Err(TPF_EINVAL, "tpf_host_dec_multi: device " + std::to_string(devs[d]) + " is not visible");
+        std::vector<uint64_t> scanned;
+        if (!h_off)
+        {
+            scanned.resize(nblocks + 1);
+            if (tpf_scan_offsets(fmt, h_in, in_bytes, n, nblocks, scanned.data()) < 0)
+                throw Err(TPF_ECORRUPT, "tpf_host_dec_multi: malformed block while scanning offsets");
+            h_off = scanned.data();
+        }
+        else
+        {
+            const int64_t bad = tpf_check_offsets(h_off, nblocks, in_bytes);
+            if (bad == -static_cast<int64_t>(nblocks) - 1)
+                throw Err(TPF_EINVAL, "tpf_host_dec_multi: h_off[nblocks] is past in_bytes");
+            if (bad < 0)
+                throw Err(TPF_EINVAL, "tpf_host_dec_multi: h_off decreases at block " + std::to_string(-bad - 1));
+        }
+        const size_t es = wide_fmt(fmt) ? 8 : 4;
+        const size_t uv = unit_values(fmt, n);
+        // shard cuts: equal shares of the stream's bytes (block granularity)
+        std::vector<uint64_t> cut(static_cast<size_t>(ndev) + 1, nblocks);
+        cut[0] = 0;
+        const uint64_t total = h_off[nblocks] - h_off[0];
+        for (int d = 1; d < ndev; ++d)
+        {
+            const uint64_t target = h_off[0] + total / static_cast<uint64_t>(ndev) * static_cast<uint64_t>(d);
+            cut[d] = std::max<uint64_t>(cut[d - 1], static_cast<uint64_t>(std::lower_bound(h_off, h_off + nblocks, target) - h_off));
+        }
+        const tpf::PerblockPause pause;
+        // one portable registration of each host range (skipped if the range
+        // is already pinned or registered); the shards' own Pin then finds it
+        struct PinAll
+        {
+            void * p = nullptr;
+            PinAll(const void * ptr, size_t bytes)
+            {
+                hipPointerAttribute_t a{};
+                if (!ptr || !bytes)
+                    return;
+                if (hipPointerGetAttributes(&a, ptr) == hipSuccess && a.type != hipMemoryTypeUnregistered)
+                    return;
+                (void)hipGetLastError();
+                if (hipHostRegister(const_cast<void *>(ptr), bytes, hipHostRegisterPortable | hipHostRegisterMapped) == hipSuccess)
+                    p = const_cast<void *>(ptr);
+                else
+                    (void)hipGetLastError();
+            }
+            ~PinAll()
+            {
+                if (p)
+                    (void)hipHostUnregister(p);
+            }
+        };
+        const PinAll pin_in(h_in, in_bytes), pin_vals(h_vals, nblocks * uv * es);
+        std::vector<int> rc(static_cast<size_t>(ndev), TPF_OK);
+        std::vector<std::string> msg(static_cast<size_t>(ndev));
+        std::vector<std::thread> th;
+        for (int d = 0; d < ndev; ++d)
+            th.emplace_back([&, d] {
+                const uint64_t b0 = cut[d], nb = cut[d + 1] - cut[d];
+                if (nb == 0)
+                    return;
+                if (hipSetDevice(devs[d]) != hipSuccess)
+                {
+                    rc[d] = TPF_EHIP;
+                    msg[d] = "hipSetDevice failed";
+                    return;
+                }
+                rc[d] = host_dec_impl(fmt, h_in, in_bytes, h_off + b0, nb, n, static_cast<uint8_t *>(h_vals) + b0 * uv * es,
+                                      h_starts ? static_cast<const uint8_t *>(h_starts) + b0 * es : nullptr, false);
+                if (rc[d] != TPF_OK)
+                    msg[d] = tpf_last_error(); // thread-local: carried to the caller's thread below
+            });
+        for (std::thread & t : th)
+            t.join();
+        for (int d = 0; d < ndev; ++d)
+            if (rc[d] != TPF_OK)
+                throw Err(rc[d], "tpf_host_dec_multi: shard " + std::to_string(d) + " (device " + std::to_string(devs[d]) + ", blocks " +
+                                     std::to_string(cut[d]) + ".." + std::to_string(cut[d + 1]) + ", block numbers below are shard-relative): " +
+                                     msg[d]);
         return TPF_OK;
     }
     catch (const Err & e)
