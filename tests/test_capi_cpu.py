@@ -53,6 +53,13 @@ def test_no_cpu_fallback_without_device(lib):
     assert rc == -3  # TPF_ENODEV
     lib.tpf_last_error.restype = ctypes.c_char_p
     assert b"no CPU fallback" in lib.tpf_last_error()
+    # the host-stream entry points (one and several GPUs) fail the same way
+    devs = (ctypes.c_int * 2)(0, 1)
+    data = (ctypes.c_uint8 * 64)()
+    vals = (ctypes.c_uint32 * 256)()
+    lib.tpf_host_dec_multi.restype = ctypes.c_int
+    assert lib.tpf_host_dec_multi(devs, 2, 2, data, ctypes.c_uint64(64), None, ctypes.c_uint64(1), 256, vals, None) == -3
+    assert b"no CPU fallback" in lib.tpf_last_error()
     lib.tpf_p4Dec256v32.restype = ctypes.c_void_p
     buf = (ctypes.c_uint8 * 64)()
     out = (ctypes.c_uint32 * 256)()
