@@ -13,3 +13,6 @@ TAG=$T WLS="c1 c3 c3chain c4 c5" bash scripts/gpu_workloads.sh 2>&1 | cut -c1-20
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${T}_c3chain_prof -o run --output-format csv -- python3 $R/bench.py --workload c3chain --steps 10 --warmup 2 --no-cpu-baseline > $R/gpurun_out/${T}_bench_c3chain_under_rocprof.json 2> $R/gpurun_out/${T}_c3chain_prof.err || { echo "c3chain rocprof rc=$?"; tail -5 $R/gpurun_out/${T}_c3chain_prof.err; exit 1; }
 TAG=$T bash $R/scripts/gpu_bench_profile.sh 2>&1 | cut -c1-300
+cd $R
+# afterwards (does not change the package): non-temporal packed-stream loads in the hot decode, C2 A/B
+LIBS="tree ablib/decpol11.so" WL=c2 ROUNDS=2 TAG=${T}_ab bash scripts/gpu_ab.sh
