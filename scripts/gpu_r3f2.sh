@@ -15,4 +15,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${T}_c3chain
 TAG=$T bash $R/scripts/gpu_bench_profile.sh 2>&1 | cut -c1-300
 cd $R
 # afterwards (does not change the package): non-temporal packed-stream loads in the hot decode, C2 A/B
-LIBS="tree ablib/decpol11.so" WL=c2 ROUNDS=2 TAG=${T}_ab bash scripts/gpu_ab.sh
+true  # (the nt-load A/B ran with r3f2)

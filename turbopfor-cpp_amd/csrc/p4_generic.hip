@@ -424,7 +424,7 @@ struct Unit4
 // Plan pass (!WRITE): sizes into off[unit] and one byte total per wave run
 // (run_tot); write pass: offsets rebuilt from the run scan (p4_scan.h).
 template <Fmt F, bool D1, bool WRITE, uint32_t NC = 3>
-__global__ __launch_bounds__(256) void k_enc_gr(const typename FmtTraits<F>::T * __restrict in, uint64_t nblocks, uint32_t n,
+__global__ __launch_bounds__(256) TPF_SGPR_ATTR void k_enc_gr(const typename FmtTraits<F>::T * __restrict in, uint64_t nblocks, uint32_t n,
                                                  const typename FmtTraits<F>::T * __restrict starts,
                                                  typename FmtTraits<F>::T start0, uint64_t * __restrict off,
                                                  uint32_t * __restrict plan, uint32_t * __restrict run_tot, const uint64_t * __restrict run_pre,
