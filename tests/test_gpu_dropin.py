@@ -418,3 +418,22 @@ def test_host_dec_multi_vs_single():
     assert b"shard" in L.tpf_last_error()
     assert L.tpf_host_dec_multi(devs.ctypes.data, 0, 2, packed.ctypes.data, len(packed), off.ctypes.data, nb, 256,
                                 back.ctypes.data, None) == -1
+
+
+def test_host_dec_multi_p4dec32():
+    """tpf_host_dec_multi on a p4Dec32 (n=127) stream: shards cut at block
+    granularity of 128-byte blocks decode through the windowed kernel, two
+    pipelines on the same device."""
+    L = capi()
+    L.tpf_host_dec_multi.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                                     ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]
+    rng = np.random.default_rng(127)
+    nb, n = 50001, 127
+    vals = rng.integers(0, 256, size=(nb, n), dtype=np.uint64).astype(np.uint32)
+    packed, off = oracle_lib.enc32_batch(vals)
+    devs = np.zeros(2, dtype=np.int32)
+    back = np.zeros_like(vals)
+    rc = L.tpf_host_dec_multi(devs.ctypes.data, 2, 0, packed.ctypes.data, len(packed), off.ctypes.data, nb, n,
+                              back.ctypes.data, None)
+    assert rc == 0, L.tpf_last_error()
+    np.testing.assert_array_equal(back, vals)
