@@ -42,6 +42,14 @@ __device__ __forceinline__ uint32_t vblen32(uint32_t x)
 #ifndef TPF_PLAN_FFBH
 #define TPF_PLAN_FFBH 1
 #endif
+// shifted suffix sums of the cost model through the histogram's LDS (one
+// write, two ds_read2) instead of four bpermutes: the plan pass waits on its
+// LDS pipe, and this drops one LDS instruction per block -- plan 1.982 ->
+// 1.836 ms per 10M C4 blocks, encode 467-471 -> 479-483 G int32/s (A/B on one
+// box, profiles/r3_enc_suffix_lds_ab.txt)
+#ifndef TPF_PLAN_SUFFIX_LDS
+#define TPF_PLAN_SUFFIX_LDS 1
+#endif
 // v_ffbh_u32(x) + 1: 0 for x == 0 (ffbh returns -1), else clz(x) + 1 = 33 - bw32(x)
 __device__ __forceinline__ uint32_t ffbh1(uint32_t x)
 {
@@ -101,6 +109,18 @@ __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist
     const uint32_t cnt = PlanHist::get(hist, t); // lane c holds cnt[c] (0 for c > 32)
 #endif
     wave_lds_sync();
+#if TPF_PLAN_SUFFIX_LDS
+    // suffix sums S(k) = #values with bw > k, then
+    // vbsum(b) = S(b) + S(b+7) + 2 S(b+15) + 3 S(b+19) + 4 S(b+25): the shifted
+    // sums come back through the histogram's LDS (one write, two ds_read2)
+    // instead of four bpermutes of cnt
+    const uint32_t incl = wave_incl_scan(cnt);
+    const uint32_t ec = __builtin_amdgcn_readlane(incl, 63) - incl; // sum_{c > t} cnt[c]
+    hist[t] = ec;                                                    // lanes >= 32 hold 0
+    wave_lds_sync();
+    const uint32_t vbsum = ec + hist[t + 7u] + 2u * hist[t + 15u] + 3u * hist[t + 19u] + 4u * hist[t + 25u]; // lanes t > 38: unused
+    wave_lds_sync();
+#else
     auto at = [&](uint32_t c) -> uint32_t {
         // ds_bpermute takes lane c mod 64 from address bits [7:2]
         const uint32_t x = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(c << 2), static_cast<int>(cnt)));
@@ -113,6 +133,7 @@ __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist
     const uint32_t tab = __builtin_amdgcn_readlane(pab, 63);
     const uint32_t ec = (tab & 0xFFFFu) - (pab & 0xFFFFu); // sum_{c > t} cnt[c]
     const uint32_t vbsum = (tab >> 16) - (pab >> 16);     // sum_{c > t} (cnt[c] + vbacc[c])
+#endif
     uint32_t key = 0xFFFFFFFFu;
     if (t < maxb)
     {

@@ -477,17 +477,31 @@ __device__ __forceinline__ PlanG plan_block_g(const typename FmtTraits<F>::T v[4
         cnt64 = uni(PlanGHist::get(hist, 64));
     }
     wave_lds_sync();
-    auto at = [&](uint32_t c) -> uint32_t {
-        // ds_bpermute takes lane c mod 64 from address bits [7:2]
-        const uint32_t x = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(c << 2), static_cast<int>(cnt)));
-        return c < 64u ? x : (c == 64u ? cnt64 : 0u);
-    };
-    const uint32_t vbacc = at(t + 7u) + 2u * at(t + 15u) + 3u * at(t + 19u) + 4u * at(t + 25u);
-    // both suffix sums in one scan (cnt <= 256 low half, cnt + vbacc <= 11*256 high half)
-    const uint32_t pab = wave_incl_scan(cnt | ((cnt + vbacc) << 16));
-    const uint32_t tab = __builtin_amdgcn_readlane(pab, 63);
-    const uint32_t ec = (tab & 0xFFFFu) - (pab & 0xFFFFu) + cnt64;
-    const uint32_t vbsum = (tab >> 16) - (pab >> 16) + cnt64;
+    uint32_t ec, vbsum;
+    if constexpr (!wide && TPF_PLAN_SUFFIX_LDS)
+    {
+        // as plan_block256: suffix sums S(k), the shifted ones through LDS
+        const uint32_t incl = wave_incl_scan(cnt);
+        ec = __builtin_amdgcn_readlane(incl, 63) - incl; // sum_{c > t} cnt[c]; 0 for lanes >= 32
+        hist[t] = ec;
+        wave_lds_sync();
+        vbsum = ec + hist[t + 7u] + 2u * hist[t + 15u] + 3u * hist[t + 19u] + 4u * hist[t + 25u]; // lanes t > 38: unused
+        wave_lds_sync();
+    }
+    else
+    {
+        auto at = [&](uint32_t c) -> uint32_t {
+            // ds_bpermute takes lane c mod 64 from address bits [7:2]
+            const uint32_t x = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(c << 2), static_cast<int>(cnt)));
+            return c < 64u ? x : (c == 64u ? cnt64 : 0u);
+        };
+        const uint32_t vbacc = at(t + 7u) + 2u * at(t + 15u) + 3u * at(t + 19u) + 4u * at(t + 25u);
+        // both suffix sums in one scan (cnt <= 256 low half, cnt + vbacc <= 11*256 high half)
+        const uint32_t pab = wave_incl_scan(cnt | ((cnt + vbacc) << 16));
+        const uint32_t tab = __builtin_amdgcn_readlane(pab, 63);
+        ec = (tab & 0xFFFFu) - (pab & 0xFFFFu) + cnt64;
+        vbsum = (tab >> 16) - (pab >> 16) + cnt64;
+    }
     uint32_t key = 0xFFFFFFFFu;
     const uint32_t bmp = pad8d(n);
     if (t < maxb)
