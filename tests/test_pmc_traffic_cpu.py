@@ -73,3 +73,18 @@ def test_round3_kernels(tmp_path):
     d64 = "void tpf::dev::k_dec128v64w<2u, false>(unsigned char const*, unsigned long)"
     d = _run(tmp_path, "c4_64", [(p64, 1), (w64, 2), (d64, 3), (PLAN, 100)], [(p64, 0), (w64, 5), (d64, 6), (PLAN, 100)], out)
     assert d["FETCH_SIZE_KiB_median"] == 6 and d["WRITE_SIZE_KiB_median"] == 11
+
+
+def test_committed_traffic_matches_these_sources():
+    """profiles/pmc_traffic.json (the roofline.traffic bench.py replays) was
+    measured on exactly the committed library sources: every workload's
+    src_md5 is turbopfor_amd.source_md5() of this tree.  A source change
+    without a new PMC pass fails here instead of silently reporting null."""
+    sys.path.insert(0, os.path.join(ROOT, "turbopfor-cpp_amd", "python"))
+    import turbopfor_amd
+    d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    assert {"c1", "c2", "c3", "c3chain", "c4", "c4_64"} <= set(d)
+    cur = turbopfor_amd.source_md5()
+    for wl, v in d.items():
+        assert v["src_md5"] == cur, wl
+        assert v["hbm_bytes_per_launch"] > 0, wl
