@@ -136,7 +136,7 @@ def checksum(t, dev, dist_on):
 # --------------------------------------------------------- profile traffic
 def src_md5():
     try:
-        return tpf.source_md5()
+        return tpf.kernel_md5()
     except OSError:
         return None
 
@@ -147,8 +147,8 @@ def pmc_traffic(workload, nblocks):
     FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM plus WRITE_SIZE, KiB ->
     bytes).  PMC counters need a rocprofv3 pass of their own, so the number is
     never measured inside this run: it is replayed only when the entry was
-    taken with the code this process runs (md5 over the library's sources,
-    turbopfor_amd.source_md5), and the source says which measurement it is.  (None, reason) otherwise."""
+    taken with the kernels this process runs (md5 over the device sources,
+    turbopfor_amd.kernel_md5), and the source says which measurement it is.  (None, reason) otherwise."""
     src = {"file": os.path.relpath(PROFILE_TRAFFIC, ROOT), "measured_in_this_run": False}
     try:
         d = json.load(open(PROFILE_TRAFFIC)).get(workload, {})
@@ -157,12 +157,12 @@ def pmc_traffic(workload, nblocks):
     if d.get("workload") != workload or int(d.get("nblocks", -1)) != nblocks:
         src["note"] = "no PMC measurement of this workload and size"
         return None, src
-    src.update({"label": d.get("label"), "src_md5": d.get("src_md5")})
-    if d.get("src_md5") is None or d.get("src_md5") != src_md5():
-        src["note"] = "PMC measurement taken with other library sources: not replayed"
+    src.update({"label": d.get("label"), "kernel_md5": d.get("kernel_md5")})
+    if d.get("kernel_md5") is None or d.get("kernel_md5") != src_md5():
+        src["note"] = "PMC measurement taken with other kernel sources: not replayed"
         return None, src
-    src["note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this workload with code built from these library sources "
-                   "(scripts/gpu_pmc_steps.sh)")
+    src["note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this workload with code built from these kernel sources "
+                   "(scripts/gpu.sh pmc:WL)")
     return d.get("hbm_bytes_per_launch"), src
 
 

@@ -5,7 +5,7 @@ FETCH_SIZE counts half the bytes of 16 B/lane streaming reads on gfx950
 (double it), WRITE_SIZE is exact for 16 B/lane stores; both are in KiB.
 
 Each entry records the md5 of the library sources the counters were taken
-with (src_md5, turbopfor_amd.source_md5) and a label: bench.py replays the
+with (kernel_md5, turbopfor_amd.kernel_md5: the device sources) and a label: bench.py replays the
 number only while it runs code built from those same sources, and says so
 (roofline.traffic_source).
 
@@ -53,7 +53,7 @@ def per_launch(path, counter, test):
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "turbopfor-cpp_amd", "python"))
-import turbopfor_amd  # noqa: E402  (source_md5 only: no GPU, no torch import)
+import turbopfor_amd  # noqa: E402  (kernel_md5 only: no GPU, no torch import)
 
 
 def main():
@@ -71,7 +71,7 @@ def main():
     hbm = (2.0 * f_kib + w_kib) * 1024.0
     d = {"workload": wl, "nblocks": nblocks, "kernel": kname,
          "FETCH_SIZE_KiB_median": f_kib, "WRITE_SIZE_KiB_median": w_kib, "launches": [nf, nw],
-         "hbm_bytes_per_launch": int(hbm), "label": label, "src_md5": turbopfor_amd.source_md5(),
+         "hbm_bytes_per_launch": int(hbm), "label": label, "kernel_md5": turbopfor_amd.kernel_md5(), "src_md5": turbopfor_amd.source_md5(),
          "correction": "hbm = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (gfx950 FETCH_SIZE halves 16B/lane reads)"}
     allv = {}
     if os.path.exists(out):

@@ -103,7 +103,7 @@ def test_bench_data_same_on_gpu_and_cpu():
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("workload", ["c3chain", "c3", "c2"])
+@pytest.mark.parametrize("workload", ["c3chain", "c3", "c2", "c5"])
 def test_bench_two_ranks_one_gpu(workload, tmp_path):
     """bench.py --gpus 2 (launcher, two ranks sharing cuda:0 over gloo: RCCL
     refuses two ranks on one device) on a small shard: rank 1's slice

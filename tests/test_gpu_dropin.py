@@ -242,6 +242,51 @@ def test_host_streams_concurrent_threads(monkeypatch):
     assert not errors, errors
 
 
+def test_host_streams_of_two_threads_overlap():
+    """host-stream calls of different threads run AT THE SAME TIME
+    (each on its own pooled pipeline); only the library's buffer frees and
+    allocations pause the per-block server.  Two threads start a decode of the
+    same pageable stream together; their call intervals must intersect, and
+    both results are exact."""
+    import threading
+    import time
+
+    L = capi()
+    L.tpf_host_dec.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                               ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]
+    unit = np.concatenate([datagen.c2_blocks(100, bw, 10, seed=21) for bw in (6, 15, 27)])
+    up, uo = oracle_lib.enc256v32_batch(unit)
+    reps = 200  # 60,000 blocks, 61 MB of values per call
+    packed = np.tile(up, reps)
+    off = np.concatenate([np.zeros(1, np.uint64)] + [uo[1:] + np.uint64(i * len(up)) for i in range(reps)])
+    nb = len(unit) * reps
+    bar = threading.Barrier(2)
+    spans, errors = [None, None], []
+
+    def work(i):
+        try:
+            back = np.empty((nb, 256), dtype=np.uint32)
+            # warm (pipeline leased and staging grown), then the timed call
+            assert L.tpf_host_dec(2, packed.ctypes.data, len(packed), off.ctypes.data, nb, 256, back.ctypes.data, None) == 0
+            bar.wait()
+            t0 = time.perf_counter()
+            assert L.tpf_host_dec(2, packed.ctypes.data, len(packed), off.ctypes.data, nb, 256, back.ctypes.data, None) == 0
+            spans[i] = (t0, time.perf_counter())
+            np.testing.assert_array_equal(back[: len(unit)], unit)
+            np.testing.assert_array_equal(back[-len(unit):], unit)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not errors, errors
+    (a0, a1), (b0, b1) = spans
+    assert max(a0, b0) < min(a1, b1), f"calls ran one after the other: {spans}"
+
+
 def test_per_block_server_concurrent_threads():
     """Eight threads share the block server's four mailboxes: every thread's
     encode -> decode round trip of its own blocks is byte-exact (oracle) and

@@ -100,6 +100,34 @@ def test_full_size_c2_sample_vs_oracle():
     assert torch.equal(out[idx_t], vals[idx_t])
 
 
+def test_full_size_c5_shard_sample_vs_oracle():
+    """C5's single-GPU shard at full size (bench.py --workload c5: 10M blocks,
+    the first half bw 8, the rest bw 16, 10% exceptions; BASELINE configs[4]
+    is 8 such shards): the GPU encoder's bytes for 4,000 sampled blocks equal
+    the oracle's, offsets step by exactly those sizes, the decoder returns the
+    sampled blocks, and the whole shard's decode equals its values."""
+    import bench_data
+
+    nb = 10_000_000
+    vals = bench_data.gen_c5(nb, 10.0, 1, torch.device(DEV))
+    packed, offs = tpf.enc256v32(vals)
+    rng = np.random.default_rng(5)
+    idx = np.sort(np.concatenate([rng.choice(nb, 3998, replace=False), [nb // 2 - 1, nb // 2]]))
+    idx = np.unique(idx)
+    idx_t = torch.from_numpy(idx).to(DEV)
+    sample = vals[idx_t].cpu().numpy().view(np.uint32)
+    exp_packed, exp_off = oracle_lib.enc256v32_batch(sample)
+    o = offs.cpu().numpy()
+    pk = packed.cpu().numpy()
+    for i, b in enumerate(idx):
+        assert np.array_equal(pk[o[b]:o[b + 1]], exp_packed[exp_off[i]:exp_off[i + 1]]), f"block {b}"
+    err = torch.zeros(1, dtype=torch.int64, device=DEV)
+    out = tpf.dec256v32(packed, offs, nb, err=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == -1
+    assert torch.equal(out, vals)
+
+
 def test_full_size_c3_sample_vs_oracle():
     """Full-size C3 (10M blocks of Zipf posting lists, per-block starts):
     p4D1Enc256v32 bytes of 4,000 sampled blocks equal the oracle's, and the

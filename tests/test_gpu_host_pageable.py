@@ -1,0 +1,146 @@
+"""Host streams on PAGEABLE caller memory next to torch's own pageable copies,
+per-block calls and a hipGraph replay ("what's weak" #1).
+
+One round-3 suite run ended with hipErrorIllegalAddress on a pageable
+host-to-device torch copy, right after the host-stream tests (pageable NumPy
+buffers) and the hipGraph test.  Up to round 3 the host streams page-locked
+and mapped the caller's pageable ranges (hipHostRegister) for the length of a
+call and released them at its end; NumPy then handed the same heap pages to
+the next arrays, which torch copied.  This test replays that sequence, many
+times and deterministically, with the block server serving per-block calls
+from another thread throughout: every host-stream call on freshly allocated
+pageable arrays, then at once pageable torch copies of new arrays of the same
+sizes (the freed pages reused), then a replay of a captured encode + decode
+graph, each result checked exactly.
+"""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+import datagen
+import oracle_lib
+
+torch = pytest.importorskip("torch")
+tpf = pytest.importorskip("turbopfor_amd")
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _abi():
+    L = tpf.lib()
+    L.tpf_host_dec.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                               ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]
+    L.tpf_host_enc.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_int,
+                               ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    L.tpf_host_dec_multi.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                                     ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]
+    L.tpf_p4Enc256v32.restype = ctypes.c_void_p
+    L.tpf_p4Enc256v32.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]
+    L.tpf_p4Dec256v32.restype = ctypes.c_void_p
+    L.tpf_p4Dec256v32.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]
+    return L
+
+
+def _graph(L, nb):
+    """A captured encode + decode of nb blocks on device buffers (as
+    tests/test_gpu_edges.py::test_hipgraph_capture_replay)."""
+    vals = torch.zeros((nb, 256), dtype=torch.int32, device=DEV)
+    cap = int(L.tpf_p4enc256v32_bound(nb))
+    packed = torch.zeros(cap, dtype=torch.uint8, device=DEV)
+    offs = torch.zeros(nb + 1, dtype=torch.int64, device=DEV)
+    wsb = int(L.tpf_p4enc256v32_workspace_size(nb))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=DEV)
+    out = torch.empty_like(vals)
+    err = torch.zeros(1, dtype=torch.int64, device=DEV)
+
+    def seq():
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        assert L.tpf_p4enc256v32_batch(vals.data_ptr(), nb, packed.data_ptr(), cap, offs.data_ptr(), ws.data_ptr(), wsb, s) == 0
+        assert L.tpf_p4dec256v32_batch(packed.data_ptr(), cap, offs.data_ptr(), nb, out.data_ptr(), err.data_ptr(), s) == 0
+
+    seq()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        seq()
+    return g, vals, out, err, (packed, offs, ws)
+
+
+def test_pageable_host_streams_then_torch_copies(monkeypatch):
+    monkeypatch.setenv("TPF_HOST_CHUNK_BYTES", str(192 * 1024))  # many pipeline chunks per call
+    L = _abi()
+    rng = np.random.default_rng(41)
+    base = np.concatenate([datagen.c2_blocks(300, bw, 10, seed=bw) for bw in (3, 9, 17, 26, 32)])
+    exp_packed, exp_off = oracle_lib.enc256v32_batch(base)
+    g, gvals, gout, gerr, _keep = _graph(L, 2000)
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(7)
+
+    stop = threading.Event()
+    errors, calls = [], [0]
+    pb = datagen.c2_blocks(8, 13, 10, seed=2)
+
+    def per_block():  # keeps the resident block server running beside everything else
+        try:
+            while not stop.is_set():
+                for v in pb:
+                    v = np.ascontiguousarray(v)
+                    buf = np.zeros(4096, np.uint8)
+                    end = L.tpf_p4Enc256v32(v.ctypes.data, 256, buf.ctypes.data)
+                    out = np.zeros(256, np.uint32)
+                    assert L.tpf_p4Dec256v32(buf.ctypes.data, 256, out.ctypes.data) == end
+                    assert np.array_equal(out, v)
+                    calls[0] += 1
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = threading.Thread(target=per_block)
+    th.start()
+    try:
+        for it in range(24):
+            nb = (300, len(base), 811, 1201)[it % 4]
+            blocks = base[:nb].copy()
+            packed = exp_packed[: exp_off[nb]].copy()
+            off = exp_off[: nb + 1].copy()
+            back = np.empty_like(blocks)
+            assert L.tpf_host_dec(2, packed.ctypes.data, len(packed), off.ctypes.data, nb, 256, back.ctypes.data,
+                                  None) == 0, L.tpf_last_error()
+            np.testing.assert_array_equal(back, blocks)
+            out = np.empty(nb * 1100 + 64, dtype=np.uint8)
+            offo = np.empty(nb + 1, dtype=np.uint64)
+            assert L.tpf_host_enc(2, blocks.ctypes.data, nb, 256, 0, None, 0, out.ctypes.data, len(out),
+                                  offo.ctypes.data) == 0, L.tpf_last_error()
+            np.testing.assert_array_equal(offo, off)
+            assert out[: off[-1]].tobytes() == packed.tobytes()
+            if it % 3 == 0:
+                back2 = np.empty_like(blocks)
+                devs = np.zeros(2, dtype=np.int32)
+                assert L.tpf_host_dec_multi(devs.ctypes.data, 2, 2, packed.ctypes.data, len(packed), off.ctypes.data,
+                                            nb, 256, back2.ctypes.data, None) == 0, L.tpf_last_error()
+                np.testing.assert_array_equal(back2, blocks)
+                del back2
+            sizes = (back.nbytes, out.nbytes, packed.nbytes, blocks.nbytes)
+            del blocks, packed, off, back, out, offo
+            # the pages of the arrays just released go straight to new arrays,
+            # copied by torch (pageable) both ways
+            for sz in sizes:
+                x = rng.integers(0, 256, sz, dtype=np.uint8)
+                d = torch.from_numpy(x).to(DEV)
+                assert np.array_equal(d.cpu().numpy(), x)
+                del d
+            bw = torch.randint(1, 33, (gvals.shape[0], 1), device=DEV, generator=gen)
+            raw = torch.randint(-(1 << 31), (1 << 31) - 1, gvals.shape, device=DEV, generator=gen, dtype=torch.int32)
+            gvals.copy_(torch.where(bw >= 32, raw, raw & ((torch.ones_like(bw) << bw) - 1).to(torch.int32)))
+            gout.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(gout, gvals), it
+            assert int(gerr.item()) == -1
+    finally:
+        stop.set()
+        th.join(timeout=60)
+    assert not th.is_alive()
+    assert not errors, errors
+    assert calls[0] > 0

@@ -94,59 +94,100 @@ void tc(int rc)
         throw Err(rc, tpf_last_error());
 }
 
-// Page-lock (and map) a host range for the duration of a call unless it
-// already is; d = the range's device address (nullptr if the device cannot
-// address it: then the range is left pageable and HIP stages the copies).
-// "Already pinned" needs BOTH ends of the range inside ONE registration: a
-// pageable array that shares its first page with another registered array
-// (malloc'd neighbours) must not be taken for pinned, or a DMA would run past
-// the registered pages.  A range whose end lies in someone else's
-// registration is not registered again (overlapping registrations), it stays
-// pageable.
-struct Pin
+// Can the copy engines (and, mapped, the kernels) use the host range
+// [p, p + bytes) as it is?  Yes when HIP knows it as ONE allocation or
+// registration: hipHostMalloc'd or caller-registered host memory (`d` = its
+// device address) or device memory.  A pageable range -- or one that only
+// shares a page with someone else's registration -- is STAGED: host threads
+// copy it into / out of the pipeline's pinned buffers.  The library never
+// page-locks caller memory.  (Until round 3 it did, hipHostRegister for the
+// length of a call: a call's registration and release of pageable pages that
+// the interpreter's heap hands to the next arrays was the one library action
+// that changed the GPU's view of caller memory, and the suspect of the r3r
+// hipErrorIllegalAddress on a later pageable torch copy)
+struct Reach
 {
-    void * p = nullptr;
+    bool direct = true;
     void * d = nullptr;
-    static bool lookup(const void * q, hipPointerAttribute_t & a)
+};
+
+bool lookup(const void * q, hipPointerAttribute_t & a)
+{
+    a = hipPointerAttribute_t{};
+    const bool ok = hipPointerGetAttributes(&a, q) == hipSuccess && a.type != hipMemoryTypeUnregistered;
+    if (!ok)
+        (void)hipGetLastError();
+    return ok;
+}
+
+Reach reach(const void * ptr, size_t bytes)
+{
+    Reach r;
+    if (!ptr || !bytes)
+        return r;
+    const uint8_t * lo = static_cast<const uint8_t *>(ptr);
+    const uint8_t * hi = lo + bytes - 1;
+    hipPointerAttribute_t a{}, b{};
+    if (!lookup(lo, a) || !lookup(hi, b))
     {
-        a = hipPointerAttribute_t{};
-        const bool ok = hipPointerGetAttributes(&a, q) == hipSuccess && a.type != hipMemoryTypeUnregistered;
-        if (!ok)
-            (void)hipGetLastError();
-        return ok;
+        r.direct = false;
+        return r;
     }
-    Pin(const void * ptr, size_t bytes)
+    if (a.type == hipMemoryTypeHost && b.type == hipMemoryTypeHost && a.hostPointer && a.hostPointer == b.hostPointer)
     {
-        if (!ptr || !bytes)
-            return;
-        const uint8_t * lo = static_cast<const uint8_t *>(ptr);
-        const uint8_t * hi = lo + bytes - 1;
-        hipPointerAttribute_t a{}, b{};
-        const bool known_lo = lookup(lo, a), known_hi = lookup(hi, b);
-        if (known_lo || known_hi)
-        {
-            if (known_lo && known_hi && a.type == hipMemoryTypeHost && b.type == hipMemoryTypeHost && a.hostPointer &&
-                a.hostPointer == b.hostPointer && a.devicePointer)
-                d = static_cast<uint8_t *>(a.devicePointer) + (lo - static_cast<const uint8_t *>(a.hostPointer));
-            return; // device memory, or not one registration: leave it to HIP
-        }
-        if (hipHostRegister(const_cast<void *>(ptr), bytes, hipHostRegisterMapped) == hipSuccess)
-        {
-            p = const_cast<void *>(ptr);
-            if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess)
-            {
-                d = nullptr;
-                (void)hipGetLastError();
-            }
-        }
-        else
-            (void)hipGetLastError();
+        if (a.devicePointer)
+            r.d = static_cast<uint8_t *>(a.devicePointer) + (lo - static_cast<const uint8_t *>(a.hostPointer));
+        return r;
     }
-    ~Pin()
+    // device (or managed) memory handed over as a host pointer: the copy engines take it as it is
+    r.direct = (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) && a.type == b.type;
+    return r;
+}
+
+// Host copies between pageable caller memory and pinned staging, split over
+// up to TPF_HOST_COPY_THREADS (default 8) threads: one core copies ~10 GB/s,
+// the link moves ~57 GB/s one way.
+void par_copy(void * dst, const void * src, size_t n)
+{
+    static const size_t nthr = [] {
+        const char * e = std::getenv("TPF_HOST_COPY_THREADS");
+        const long v = e ? std::strtol(e, nullptr, 10) : 8;
+        return static_cast<size_t>(std::clamp<long>(v, 1, 64));
+    }();
+    constexpr size_t kPiece = 4u << 20;
+    const size_t nt = std::min(nthr, std::max<size_t>(1, n / kPiece));
+    if (nt <= 1)
     {
-        if (p)
-            (void)hipHostUnregister(p);
+        std::memcpy(dst, src, n);
+        return;
     }
+    const size_t per = ((n + nt - 1) / nt + 4095) & ~size_t(4095);
+    std::vector<std::thread> th;
+    th.reserve(nt);
+    for (size_t o = per; o < n; o += per)
+        th.emplace_back([=] { std::memcpy(static_cast<uint8_t *>(dst) + o, static_cast<const uint8_t *>(src) + o, std::min(per, n - o)); });
+    std::memcpy(dst, src, std::min(per, n));
+    for (std::thread & t : th)
+        t.join();
+}
+
+// The per-block server must not run while HIP frees, allocates or tears down
+// the library's own buffers and streams (HIP waits for every stream of the
+// device there, the server's included), so those -- and only those -- hold
+// tpf::PerblockPause.  Host-stream calls of different threads otherwise run
+// concurrently (the whole call used to hold it).  Reentrant per thread.
+thread_local int t_pause_depth = 0;
+struct FreePause
+{
+    std::optional<tpf::PerblockPause> p;
+    FreePause()
+    {
+        if (t_pause_depth++ == 0)
+            p.emplace();
+    }
+    ~FreePause() { --t_pause_depth; }
+    FreePause(const FreePause &) = delete;
+    FreePause & operator=(const FreePause &) = delete;
 };
 
 // A grow-only device (or pinned host) buffer.
@@ -160,6 +201,7 @@ struct Buf
     {
         if (n <= cap && p)
             return p;
+        const FreePause fp;
         release();
         n = std::max<size_t>(n, 256);
         if (host)
@@ -172,7 +214,10 @@ struct Buf
     void release()
     {
         if (p)
+        {
+            const FreePause fp;
             (void)(host ? hipHostFree(p) : hipFree(p));
+        }
         p = nullptr;
         cap = 0;
     }
@@ -181,11 +226,19 @@ struct Buf
 
 // One pipeline slot: per-chunk buffers; events: `up` = the chunk's uploads
 // landed (copy stream), `mid` = encode offsets reached the host, `done` = the
-// kernel stream finished with the slot.
+// kernel stream finished with the slot.  hin / hout / hst: pinned staging of
+// pageable caller ranges; `pend` = the host copy-out of a staged result,
+// done once `done` has completed.
 struct Slot
 {
     hipEvent_t up = nullptr, mid = nullptr, done = nullptr;
-    Buf in, vals, ws, start, off, hoff{true};
+    Buf in, vals, ws, start, off, hoff{true}, hin{true}, hout{true}, hst{true};
+    struct Pending
+    {
+        void * dst = nullptr;
+        const void * src = nullptr;
+        size_t n = 0;
+    } pend;
     Slot()
     {
         for (hipEvent_t * e : {&up, &mid, &done})
@@ -197,6 +250,14 @@ struct Slot
             if (e)
                 (void)hipEventDestroy(e);
     }
+    // wait until the kernel stream is done with the slot, then finish its staged copy-out
+    void drain()
+    {
+        hc(hipEventSynchronize(done), "wait slot");
+        if (pend.n)
+            par_copy(pend.dst, pend.src, pend.n);
+        pend = Pending{};
+    }
 };
 
 struct Pipeline
@@ -204,7 +265,8 @@ struct Pipeline
     int dev = -1;
     hipStream_t cs = nullptr, ks = nullptr; // copy stream, kernel stream
     Slot slots[kSlots];
-    Buf errs; // decode: one first-inconsistent-block word per chunk, read back once at the end
+    Buf errs;          // decode: one first-inconsistent-block word per chunk, read back once at the end
+    Buf herrs{true};   // their pinned host copy
     explicit Pipeline(int d) : dev(d)
     {
         hc(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "stream");
@@ -247,6 +309,8 @@ struct Lease
         }
         if (!p)
             p = new Pipeline(dev);
+        for (Slot & s : p->slots)
+            s.pend = Slot::Pending{};
     }
     ~Lease()
     {
@@ -257,7 +321,10 @@ struct Lease
             g_pool.push_back(p);
         }
         else
+        {
+            const FreePause fp;
             delete p;
+        }
     }
 };
 
@@ -275,7 +342,7 @@ void need_device()
 }
 
 int host_dec_impl(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_t * h_off, uint64_t nblocks, unsigned n,
-                  void * h_vals, const void * h_starts, bool take_pause);
+                  void * h_vals, const void * h_starts);
 
 } // namespace
 
@@ -288,7 +355,7 @@ extern "C" {
 int tpf_host_dec(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_t * h_off, uint64_t nblocks, unsigned n,
                  void * h_vals, const void * h_starts)
 {
-    return host_dec_impl(fmt, h_in, in_bytes, h_off, nblocks, n, h_vals, h_starts, true);
+    return host_dec_impl(fmt, h_in, in_bytes, h_off, nblocks, n, h_vals, h_starts);
 }
 
 } // extern "C"
@@ -296,20 +363,13 @@ int tpf_host_dec(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_
 namespace
 {
 int host_dec_impl(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_t * h_off, uint64_t nblocks, unsigned n,
-                  void * h_vals, const void * h_starts, bool take_pause)
+                  void * h_vals, const void * h_starts)
 {
     try
     {
         if (nblocks == 0)
             return TPF_OK;
         need_device();
-        // the resident per-block server stays stopped (and per-block calls
-        // wait) for the whole call: HIP's frees, host (un)registrations and
-        // device-wide waits would otherwise wait on the server's stream
-        // (tpf_host_dec_multi holds it once for all its shards)
-        std::optional<tpf::PerblockPause> pause;
-        if (take_pause)
-            pause.emplace();
         std::vector<uint64_t> scanned;
         if (!h_off)
         {
@@ -330,8 +390,11 @@ int host_dec_impl(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64
         const size_t es = wide_fmt(fmt) ? 8 : 4;
         const size_t uv = unit_values(fmt, n);
         const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(nblocks, chunk_value_bytes() / (es * uv)));
-        Pin pin_in(h_in, in_bytes), pin_vals(h_vals, nblocks * uv * es);
-        uint8_t * dv = sdma_down() ? nullptr : static_cast<uint8_t *>(pin_vals.d);
+        // only this call's byte range of h_in (a shard of tpf_host_dec_multi reads no more)
+        const Reach r_in = reach(h_in + h_off[0], h_off[nblocks] - h_off[0]);
+        const Reach r_vals = reach(h_vals, nblocks * uv * es);
+        const Reach r_st = h_starts ? reach(h_starts, nblocks * es) : Reach{};
+        uint8_t * dv = (sdma_down() || !r_vals.direct) ? nullptr : static_cast<uint8_t *>(r_vals.d);
         size_t max_in = 0;
         for (uint64_t c0 = 0; c0 < nblocks; c0 += chunk)
         {
@@ -345,11 +408,12 @@ int host_dec_impl(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64
         // (a small device-to-host copy per chunk can stall the host loop)
         const uint64_t nchunks = (nblocks + chunk - 1) / chunk;
         auto * d_errs = static_cast<uint64_t *>(P.errs.get(nchunks * 8));
+        auto * h_errs = static_cast<uint64_t *>(P.herrs.get(nchunks * 8));
         uint64_t k = 0;
         for (uint64_t c0 = 0; c0 < nblocks; c0 += chunk, ++k)
         {
             Slot & sl = P.slots[k % kSlots];
-            hc(hipEventSynchronize(sl.done), "wait slot"); // chunk k-kSlots is done with the slot
+            sl.drain(); // chunk k-kSlots is done with the slot (and its staged values are out)
             const uint64_t c1 = std::min(nblocks, c0 + chunk);
             const uint64_t nb = c1 - c0;
             const uint64_t b0 = h_off[c0], bytes = h_off[c1] - b0;
@@ -360,28 +424,53 @@ int host_dec_impl(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64
             void * out = dv ? static_cast<void *>(dv + c0 * uv * es) : sl.vals.get(chunk * uv * es);
             for (uint64_t i = 0; i <= nb; ++i)
                 st_off[i] = h_off[c0 + i] - b0;
+            const void * src_in = h_in + b0;
+            if (!r_in.direct)
+            {
+                void * s = sl.hin.get(max_in + 64);
+                par_copy(s, src_in, bytes);
+                src_in = s;
+            }
             hc(hipMemcpyAsync(d_off, st_off, (nb + 1) * 8, hipMemcpyHostToDevice, P.cs), "H2D off");
-            hc(hipMemcpyAsync(d_in, h_in + b0, bytes, hipMemcpyHostToDevice, P.cs), "H2D bytes");
+            hc(hipMemcpyAsync(d_in, src_in, bytes, hipMemcpyDefault, P.cs), "H2D bytes");
             if (h_starts)
-                hc(hipMemcpyAsync(d_start, static_cast<const uint8_t *>(h_starts) + c0 * es, nb * es, hipMemcpyHostToDevice, P.cs),
-                   "H2D starts");
+            {
+                const void * src_st = static_cast<const uint8_t *>(h_starts) + c0 * es;
+                if (!r_st.direct)
+                {
+                    void * s = sl.hst.get(chunk * es);
+                    std::memcpy(s, src_st, nb * es);
+                    src_st = s;
+                }
+                hc(hipMemcpyAsync(d_start, src_st, nb * es, hipMemcpyDefault, P.cs), "H2D starts");
+            }
             hc(hipEventRecord(sl.up, P.cs), "record up");
             hc(hipStreamWaitEvent(P.ks, sl.up, 0), "wait up");
             tc(tpf_dec_batch(fmt, d_in, bytes, d_off, nb, n, out, d_start, d_errs + k, P.ks));
             if (!dv)
-                hc(hipMemcpyAsync(static_cast<uint8_t *>(h_vals) + c0 * uv * es, out, nb * uv * es, hipMemcpyDeviceToHost, P.ks),
-                   "D2H vals");
+            {
+                uint8_t * dst = static_cast<uint8_t *>(h_vals) + c0 * uv * es;
+                if (r_vals.direct)
+                    hc(hipMemcpyAsync(dst, out, nb * uv * es, hipMemcpyDefault, P.ks), "D2H vals");
+                else
+                {
+                    void * s = sl.hout.get(chunk * uv * es);
+                    hc(hipMemcpyAsync(s, out, nb * uv * es, hipMemcpyDeviceToHost, P.ks), "D2H vals");
+                    sl.pend = {dst, s, nb * uv * es};
+                }
+            }
             hc(hipEventRecord(sl.done, P.ks), "record done");
         }
-        std::vector<uint64_t> errs(nchunks);
-        hc(hipMemcpyAsync(errs.data(), d_errs, nchunks * 8, hipMemcpyDeviceToHost, P.ks), "D2H errs");
+        hc(hipMemcpyAsync(h_errs, d_errs, nchunks * 8, hipMemcpyDeviceToHost, P.ks), "D2H errs");
         hc(hipStreamSynchronize(P.ks), "sync");
+        for (Slot & sl : P.slots)
+            sl.drain();
         lease.ok = true;
         uint64_t bad = ~0ull; // first block whose parsed length disagrees with its offsets
         for (uint64_t i = 0; i < nchunks; ++i)
-            if (errs[i] != ~0ull)
+            if (h_errs[i] != ~0ull)
             {
-                bad = i * chunk + errs[i];
+                bad = i * chunk + h_errs[i];
                 break;
             }
         if (bad != ~0ull)
@@ -406,8 +495,8 @@ extern "C" {
 // GPUs"): the blocks are cut into ndev contiguous shards of about equal
 // bytes, and shard d runs tpf_host_dec's pipeline on device devs[d] from a
 // thread of its own (each device has its own PCIe link and copy engines).
-// The input and output ranges are registered once, portable, for all
-// devices; the per-block servers stay paused for the whole call.
+// Each shard reaches (or stages) only its own byte range of the input and its
+// own values.
 int tpf_host_dec_multi(const int * devs, int ndev, int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64_t * h_off,
                        uint64_t nblocks, unsigned n, void * h_vals, const void * h_starts)
 {
@@ -450,32 +539,6 @@ int tpf_host_dec_multi(const int * devs, int ndev, int fmt, const uint8_t * h_in
             const uint64_t target = h_off[0] + total / static_cast<uint64_t>(ndev) * static_cast<uint64_t>(d);
             cut[d] = std::max<uint64_t>(cut[d - 1], static_cast<uint64_t>(std::lower_bound(h_off, h_off + nblocks, target) - h_off));
         }
-        const tpf::PerblockPause pause;
-        // one portable registration of each host range (skipped if the range
-        // is already pinned or registered); the shards' own Pin then finds it
-        struct PinAll
-        {
-            void * p = nullptr;
-            PinAll(const void * ptr, size_t bytes)
-            {
-                hipPointerAttribute_t a{};
-                if (!ptr || !bytes)
-                    return;
-                if (hipPointerGetAttributes(&a, ptr) == hipSuccess && a.type != hipMemoryTypeUnregistered)
-                    return;
-                (void)hipGetLastError();
-                if (hipHostRegister(const_cast<void *>(ptr), bytes, hipHostRegisterPortable | hipHostRegisterMapped) == hipSuccess)
-                    p = const_cast<void *>(ptr);
-                else
-                    (void)hipGetLastError();
-            }
-            ~PinAll()
-            {
-                if (p)
-                    (void)hipHostUnregister(p);
-            }
-        };
-        const PinAll pin_in(h_in, in_bytes), pin_vals(h_vals, nblocks * uv * es);
         std::vector<int> rc(static_cast<size_t>(ndev), TPF_OK);
         std::vector<std::string> msg(static_cast<size_t>(ndev));
         std::vector<std::thread> th;
@@ -491,7 +554,7 @@ int tpf_host_dec_multi(const int * devs, int ndev, int fmt, const uint8_t * h_in
                     return;
                 }
                 rc[d] = host_dec_impl(fmt, h_in, in_bytes, h_off + b0, nb, n, static_cast<uint8_t *>(h_vals) + b0 * uv * es,
-                                      h_starts ? static_cast<const uint8_t *>(h_starts) + b0 * es : nullptr, false);
+                                      h_starts ? static_cast<const uint8_t *>(h_starts) + b0 * es : nullptr);
                 if (rc[d] != TPF_OK)
                     msg[d] = tpf_last_error(); // thread-local: carried to the caller's thread below
             });
@@ -529,12 +592,12 @@ int tpf_host_enc(int fmt, const void * h_vals, uint64_t nblocks, unsigned n, int
         if (nblocks == 0)
             return TPF_OK;
         need_device();
-        const tpf::PerblockPause pause; // as tpf_host_dec
         const size_t es = wide_fmt(fmt) ? 8 : 4;
         const size_t uv = unit_values(fmt, n);
         const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(nblocks, chunk_value_bytes() / (es * uv)));
-        Pin pin_vals(h_vals, nblocks * uv * es), pin_out(h_out, out_cap);
-        uint8_t * dout = sdma_down() ? nullptr : static_cast<uint8_t *>(pin_out.d);
+        const Reach r_vals = reach(h_vals, nblocks * uv * es), r_out = reach(h_out, out_cap);
+        const Reach r_st = (d1 && h_starts) ? reach(h_starts, nblocks * es) : Reach{};
+        uint8_t * dout = (sdma_down() || !r_out.direct) ? nullptr : static_cast<uint8_t *>(r_out.d);
         const size_t cap = tpf_enc_bound(fmt, chunk, n);
         const size_t wsb = std::max<size_t>(tpf_enc_workspace_size(fmt, chunk, n), 256);
         Lease lease;
@@ -554,8 +617,14 @@ int tpf_host_enc(int fmt, const void * h_vals, uint64_t nblocks, unsigned n, int
                 h_off[c0 + i] = pos + st_off[i];
             if (dout)
                 tc(tpf_copy_async(dout + pos, sl.in.p, total, P.ks));
+            else if (r_out.direct)
+                hc(hipMemcpyAsync(h_out + pos, sl.in.p, total, hipMemcpyDefault, P.ks), "D2H bytes");
             else
-                hc(hipMemcpyAsync(h_out + pos, sl.in.p, total, hipMemcpyDeviceToHost, P.ks), "D2H bytes");
+            {
+                void * st = sl.hout.get(cap);
+                hc(hipMemcpyAsync(st, sl.in.p, total, hipMemcpyDeviceToHost, P.ks), "D2H bytes");
+                sl.pend = {h_out + pos, st, total};
+            }
             hc(hipEventRecord(sl.done, P.ks), "record done");
             pos += total;
         };
@@ -563,7 +632,7 @@ int tpf_host_enc(int fmt, const void * h_vals, uint64_t nblocks, unsigned n, int
         for (uint64_t c0 = 0; c0 < nblocks; c0 += chunk, ++k)
         {
             Slot & sl = P.slots[k % kSlots];
-            hc(hipEventSynchronize(sl.done), "wait slot");
+            sl.drain(); // chunk k-kSlots is done with the slot (and its staged bytes are out)
             c0s.push_back(c0);
             const uint64_t nb = std::min(nblocks, c0 + chunk) - c0;
             auto * d_pk = static_cast<uint8_t *>(sl.in.get(cap));
@@ -571,15 +640,27 @@ int tpf_host_enc(int fmt, const void * h_vals, uint64_t nblocks, unsigned n, int
             void * d_ws = sl.ws.get(wsb);
             auto * d_off = static_cast<uint64_t *>(sl.off.get((chunk + 1) * 8));
             void * st_off = sl.hoff.get((chunk + 1) * 8);
-            hc(hipMemcpyAsync(d_vals, static_cast<const uint8_t *>(h_vals) + c0 * uv * es, nb * uv * es, hipMemcpyHostToDevice, P.cs),
-               "H2D vals");
+            const void * src_vals = static_cast<const uint8_t *>(h_vals) + c0 * uv * es;
+            if (!r_vals.direct)
+            {
+                void * st = sl.hin.get(chunk * uv * es);
+                par_copy(st, src_vals, nb * uv * es);
+                src_vals = st;
+            }
+            hc(hipMemcpyAsync(d_vals, src_vals, nb * uv * es, hipMemcpyDefault, P.cs), "H2D vals");
             const void * dstart = nullptr;
             uint64_t s0 = start0;
             if (d1 && h_starts)
             {
                 void * d_start = sl.start.get(chunk * es);
-                hc(hipMemcpyAsync(d_start, static_cast<const uint8_t *>(h_starts) + c0 * es, nb * es, hipMemcpyHostToDevice, P.cs),
-                   "H2D starts");
+                const void * src_st = static_cast<const uint8_t *>(h_starts) + c0 * es;
+                if (!r_st.direct)
+                {
+                    void * st = sl.hst.get(chunk * es);
+                    std::memcpy(st, src_st, nb * es);
+                    src_st = st;
+                }
+                hc(hipMemcpyAsync(d_start, src_st, nb * es, hipMemcpyDefault, P.cs), "H2D starts");
                 dstart = d_start;
             }
             else if (d1 && c0 > 0)
@@ -600,6 +681,8 @@ int tpf_host_enc(int fmt, const void * h_vals, uint64_t nblocks, unsigned n, int
         }
         finish(k - 1);
         hc(hipStreamSynchronize(P.ks), "sync");
+        for (Slot & sl : P.slots)
+            sl.drain();
         lease.ok = true;
         return TPF_OK;
     }
@@ -615,7 +698,7 @@ int tpf_host_enc(int fmt, const void * h_vals, uint64_t nblocks, unsigned n, int
 
 void tpf_host_release(void)
 {
-    const tpf::PerblockPause pause; // the frees below wait on every stream of the device
+    const FreePause fp; // the frees below wait on every stream of the device
     std::vector<Pipeline *> idle;
     {
         std::lock_guard<std::mutex> g(g_pool_mu);

@@ -30,24 +30,39 @@ def build():
     subprocess.check_call(["make", "-s", "-C", PKG_DIR, f"-j{min(os.cpu_count() or 4, 16)}"])
 
 
-def source_md5():
-    """md5 over the library's sources (turbopfor-cpp_amd/csrc/*, its Makefile
-    and include/*.h, sorted by path; path and contents): the identity of the
-    code a PMC measurement was taken with.  (The built .so's own bytes differ
-    when the same sources are rebuilt elsewhere -- e.g. a build on the GPU box
-    embeds that box's paths -- so they do not identify the code.)"""
+def _md5(files, root):
     import hashlib
 
-    root = os.path.dirname(PKG_DIR)
-    files = [os.path.join(PKG_DIR, "Makefile")]
-    for d in (os.path.join(PKG_DIR, "csrc"), os.path.join(root, "include")):
-        files += [os.path.join(d, f) for f in os.listdir(d) if f.endswith((".h", ".hip", ".cpp"))]
     h = hashlib.md5()
     for f in sorted(files):
         h.update(os.path.relpath(f, root).encode() + b"\0")
         with open(f, "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()
+
+
+def source_md5():
+    """md5 over the library's sources (turbopfor-cpp_amd/csrc/*, its Makefile
+    and include/*.h, sorted by path; path and contents): the identity of the
+    build (build_stamp.json).  (The built .so's own bytes differ when the same
+    sources are rebuilt elsewhere -- e.g. a build on the GPU box embeds that
+    box's paths -- so they do not identify the code.)"""
+    root = os.path.dirname(PKG_DIR)
+    files = [os.path.join(PKG_DIR, "Makefile")]
+    for d in (os.path.join(PKG_DIR, "csrc"), os.path.join(root, "include")):
+        files += [os.path.join(d, f) for f in os.listdir(d) if f.endswith((".h", ".hip", ".cpp"))]
+    return _md5(files, root)
+
+
+def kernel_md5():
+    """md5 over the DEVICE code only (csrc/*.hip, csrc/*.h, the Makefile's
+    flags): the identity of the kernels a PMC traffic measurement was taken
+    with.  Host-side edits (host_api.cpp, host_stream.cpp, include/) do not
+    change what a kernel moves, so they do not invalidate the measurement."""
+    root = os.path.dirname(PKG_DIR)
+    d = os.path.join(PKG_DIR, "csrc")
+    files = [os.path.join(PKG_DIR, "Makefile")] + [os.path.join(d, f) for f in os.listdir(d) if f.endswith((".h", ".hip"))]
+    return _md5(files, root)
 
 
 def lib():
