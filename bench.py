@@ -867,6 +867,176 @@ def run_c4(args, world, rank, dev, T):
                 cpu), ok_all
 
 
+def cpu_baseline_d1enc(vals_host, starts_host, nblocks, budget_s=12.0, threads=None):
+    """C3 encode CPU baseline: the reference library (oracle/_ref) writing the
+    first 1/8 of the same posting list with turbopfor::scalar::p4D1Enc256v32,
+    each thread chained through the returned end pointers and the previous
+    block's last value (README.md:108-123).  None when oracle/_ref is absent."""
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libtpref.so")
+    if not os.path.exists(ref_so):
+        return None
+    threads, host = cpu_host() if threads is None else (threads, {"threads_used": threads})
+    nb = max(1, nblocks // 8)
+    v = np.ascontiguousarray(vals_host[:nb], dtype=np.uint32)
+    st = np.ascontiguousarray(starts_host[:nb], dtype=np.uint32)
+    slot = 1088
+    scratch = np.empty(nb * slot + 64, dtype=np.uint8)
+    off = np.empty(nb, dtype=np.uint64)
+    L = ctypes.CDLL(ref_so)
+    f = L.tpref_d1enc256v32_stream_mt
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                  ctypes.c_int, ctypes.c_int]
+    f.restype = ctypes.c_double
+    run = lambda disp: f(v.ctypes.data, st.ctypes.data, nb, scratch.ctypes.data, slot, off.ctypes.data, threads, disp)
+    tot, reps = _timed_reps(lambda: run(0), budget_s)
+    dtot, dreps = _timed_reps(lambda: run(1), budget_s / 3)
+    return {"value": round(nb * 256 * reps / tot / 1e9, 3), "unit": "G int32/s", "cores": threads, "kind": "reference",
+            "host": host, "avx2_dispatch": {"value": round(nb * 256 * dreps / dtot / 1e9, 3)},
+            "sample": f"first {nb} blocks of the same C3 list x {reps} passes, {threads} threads, "
+                      f"turbopfor::scalar::p4D1Enc256v32 chained (reference scalar, oracle/_ref) on {_cpu_model()}"}
+
+
+def run_c3enc(args, world, rank, dev, T):
+    """p4D1Enc256v32 on the C3 posting list (the encoder's
+    vbyte-heavy case): one chained list per rank-shard, written the way a
+    reference caller writes it (block i starts from block i-1's last value:
+    start0 + the values themselves, tpf_p4d1enc256v32_batch with no starts).
+    Verified: the per-block-start encoding of the same values is identical and
+    decode(encode(x)) == x."""
+    nb = args.nblocks
+    first = shard_of(nb, world, rank)
+    carry = (lambda tot: tpf_shard.exclusive_prefix(tot, dev)) if T.dist_on else None
+    vals, starts = gen_c3(nb, seed=7, dev=dev, first_block=first, carry_fn=carry)
+    start0 = int(starts[0].item()) & 0xFFFFFFFF
+    cap = int(tpf.lib().tpf_p4enc256v32_bound(nb))
+    enc_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    state = {}
+
+    def enc():
+        state["p"], state["o"] = tpf.enc256v32(vals, d1=True, start0=start0, out=enc_out)
+
+    elapsed, kern_ms = T.run(enc, args.steps, args.warmup)
+    p1, o1 = state["p"], state["o"]
+    pbytes = int(o1[-1].item())
+    p2, o2 = tpf.enc256v32(vals, d1=True, starts=starts)
+    ok = bool(torch.equal(o1, o2)) and bool(torch.equal(p1[:pbytes], p2[:pbytes]))
+    del p2, o2
+    out = tpf.dec256v32(p1, o1, nb, starts=starts)
+    ok = ok and bool(torch.equal(out, vals))
+    del out
+    if T.dist_on:
+        ok = tpf_shard.all_ok(ok, dev)
+    avg_ms = float(np.mean(kern_ms))
+    alg = nb * (1024 + 8) + pbytes + 8
+    per_rank = per_rank_stats(world, dev, avg_ms, alg / (avg_ms * 1e-3) / 1e9)
+    if rank != 0:
+        return None
+    value = nb * 256 * world / (elapsed / args.steps) / 1e9
+    roof = {"bound": "hbm", "achieved": round(alg / (avg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), **traffic_fields("c3enc", nb),
+            "kernel": "k_enc256v32_plan<D1> + run scan (2 small kernels) + k_enc256v32_write<D1>",
+            "kernel_ms_avg": round(avg_ms, 4), "alg_bytes_per_launch": int(alg),
+            "alg_bytes_def": "1024 B values + block bytes + 8 B offset per block (the write pass's second read of the "
+                             "values is not counted)",
+            "per_rank": per_rank}
+    cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_d1enc(
+        vals.cpu().numpy().view(np.uint32), starts.cpu().numpy().view(np.uint32), nb)
+    cfg = {"workload": "C3 encode: p4D1Enc256v32 of the C3 Zipf posting list, chained (start0 + the list itself)",
+           "nblocks_per_gpu": nb, "bytes_per_int": round(pbytes / nb / 256, 4), **block_mix(p1, o1),
+           "parallelism": f"shard{world}", "shard_blocks": [first, first + nb], "verified": ok}
+    return line("G int32/s device-resident p4D1Enc256v32 (chained posting list)", value, "G int32/s", world, args.steps,
+                args.warmup, elapsed, "u32", "synthetic (GPU-generated C3 posting list; encoding checked against the "
+                "per-block-start encoder and decoded back: " + ("ok" if ok else "MISMATCH") + ")", cfg, roof, cpu), ok
+
+
+def cpu_baseline_d1dec64(packed_host, off_host, starts_host, nunits, budget_s=12.0, threads=None):
+    """64-bit chained list CPU baseline: the reference library (oracle/_ref)
+    running turbopfor::scalar::p4D1Dec256v64 over the first 1/8 of the same
+    stream, each thread chained through the previous unit's last value."""
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libtpref.so")
+    if not os.path.exists(ref_so):
+        return None
+    threads, host = cpu_host() if threads is None else (threads, {"threads_used": threads})
+    nb = max(1, nunits // 8)
+    b1 = int(off_host[nb])
+    sample = np.concatenate([packed_host[:b1], np.zeros(64, np.uint8)])
+    soff = np.ascontiguousarray(off_host[: nb + 1], dtype=np.uint64)
+    st = np.ascontiguousarray(starts_host[:nb], dtype=np.uint64)
+    out = np.empty((nb, 256), dtype=np.uint64)
+    L = ctypes.CDLL(ref_so)
+    f = L.tpref_d1dec256v64_stream_mt
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
+                  ctypes.c_int, ctypes.c_int]
+    f.restype = ctypes.c_double
+    run = lambda disp: f(sample.ctypes.data, soff.ctypes.data, st.ctypes.data, nb, out.ctypes.data, threads, disp, 1)
+    tot, reps = _timed_reps(lambda: run(0), budget_s)
+    exp = out.copy()
+    dtot, dreps = _timed_reps(lambda: run(1), budget_s / 3)
+    return {"value": round(nb * 256 * reps / tot / 1e9, 3), "unit": "G int64/s", "cores": threads, "kind": "reference",
+            "host": host, "avx2_dispatch": {"value": round(nb * 256 * dreps / dtot / 1e9, 3),
+                                            "units_differing_from_scalar": int((out != exp).any(axis=1).sum())},
+            "sample": f"first {nb} units of the same stream x {reps} passes, {threads} threads, "
+                      f"turbopfor::scalar::p4D1Dec256v64 chained through each unit's last value (oracle/_ref) on {_cpu_model()}"}
+
+
+def run_c3chain64(args, world, rank, dev, T):
+    """A 64-bit chained posting list (SURVEY §8 f1 widened to
+    256v64): the C3 gaps as u64 ids above 2^32, p4D1Enc256v64 units chained the
+    way reference callers chain them; decoded from start0 alone by
+    tpf_d1dec64_chain_sums (unit totals + u64 run scan) and
+    tpf_d1dec64_chain_decode.  Across ranks: one u64 total per rank all-gathered
+    (tpf_shard.chained_base64)."""
+    nb = args.nblocks
+    first = shard_of(nb, world, rank)
+    carry = (lambda tot: tpf_shard.exclusive_prefix(tot, dev)) if T.dist_on else None
+    vals, starts = bench_data.gen_c3_64(nb, seed=7, dev=dev, first_block=first, carry_fn=carry)
+    packed, offs = tpf.enc_batch("256v64", vals.view(-1), nb, 256, d1=True, starts=starts)
+    pbytes = int(packed.numel())
+    L = tpf.lib()
+    fmt = tpf.FMT["256v64"]
+    ws = torch.empty(int(L.tpf_d1dec64_chain_workspace_size(nb)), dtype=torch.uint8, device=dev)
+    total = torch.zeros(1, dtype=torch.int64, device=dev)
+    out = torch.empty((nb, 256), dtype=torch.int64, device=dev)
+    start0 = (1 << 40) + 12345  # the value before the GLOBAL list's first unit
+
+    def step():
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        assert L.tpf_d1dec64_chain_sums(fmt, packed.data_ptr(), pbytes, offs.data_ptr(), nb, ws.data_ptr(), ws.numel(),
+                                        total.data_ptr(), None, s) == 0
+        base = tpf_shard.chained_base64(total, start0=start0) if T.dist_on else start0
+        assert L.tpf_d1dec64_chain_decode(fmt, packed.data_ptr(), pbytes, offs.data_ptr(), nb, out.data_ptr(),
+                                          ctypes.c_uint64(base), ws.data_ptr(), None, s) == 0
+
+    elapsed, kern_ms = T.run(step, args.steps, args.warmup)
+    ok = bool(torch.equal(out, vals))
+    if T.dist_on:
+        ok = tpf_shard.all_ok(ok, dev)
+    _, plain_ms = T.run(lambda: tpf.dec_batch("256v64", packed, offs, nb, 256, starts=starts, out=out.view(-1)), 5, 1)
+    ok = ok and bool(torch.equal(out, vals))
+    avg_ms = float(np.mean(kern_ms))
+    alg = pbytes + nb * (2048 + 8) + 8
+    per_rank = per_rank_stats(world, dev, avg_ms, alg / (avg_ms * 1e-3) / 1e9)
+    if rank != 0:
+        return None
+    value = nb * 256 * world / (elapsed / args.steps) / 1e9
+    roof = {"bound": "hbm", "achieved": round(alg / (avg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), **traffic_fields("c3chain64", nb),
+            "kernel": "k_dec128v64w<2, Sum> + run scan (u64) + k_dec128v64w<2, Prefix>", "kernel_ms_avg": round(avg_ms, 4),
+            "alg_bytes_per_launch": int(alg),
+            "alg_bytes_def": "unit bytes + 2048 B decoded + 8 B offset per unit (phase A's read of the stream not counted)",
+            "per_unit_starts_ms_avg": round(float(np.mean(plain_ms)), 4), "per_rank": per_rank}
+    cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_d1dec64(
+        packed.cpu().numpy(), offs.cpu().numpy().astype(np.uint64), starts.cpu().numpy().view(np.uint64), nb)
+    cfg = {"workload": "C3 as a 64-bit chained list: p4D1Dec256v64 units of the C3 Zipf gaps as u64 ids above 2^32, "
+                       "decoded from start0 alone",
+           "nunits_per_gpu": nb, "bytes_per_int": round(pbytes / nb / 256, 4), "parallelism": f"shard{world}",
+           "shard_units": [first, first + nb], "verified": ok,
+           "per_unit_starts_G_int64_per_s": round(nb * 256 / (float(np.mean(plain_ms)) * 1e-3) / 1e9, 2)}
+    return line("G int64/s device-resident p4D1Dec256v64 (chained list)", value, "G int64/s", world, args.steps,
+                args.warmup, elapsed, "u64", "synthetic (GPU-generated 64-bit posting list, GPU-encoded; chained decode "
+                "verified bit-exact on every rank: " + ("ok" if ok else "MISMATCH") + ")", cfg, roof, cpu), ok
+
+
 def cpu_abtest_c1(vals_host, blk_host, blen, n):
     """ab_test methodology (benchmarks/ab_test.cpp:553-701) on the reference
     library built from its own sources (oracle/_ref): one L1-hot block,
@@ -976,7 +1146,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--nblocks", type=int, default=10_000_000, help="blocks per GPU (shard)")
     ap.add_argument("--exc", type=float, default=10.0)
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c3chain", "c4", "c5", "sweep"])
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c3chain", "c3enc", "c3chain64", "c4", "c5", "sweep"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="c2: also measure the pinned host-memory path")
     ap.add_argument("--no-probes", action="store_true", help="c2: skip the in-run HBM read/write/copy probes")
@@ -1027,6 +1197,10 @@ def main():
         res = run_c3(args, world, rank, dev, T, chained=False)
     elif args.workload == "c3chain":
         res = run_c3(args, world, rank, dev, T, chained=True)
+    elif args.workload == "c3enc":
+        res = run_c3enc(args, world, rank, dev, T)
+    elif args.workload == "c3chain64":
+        res = run_c3chain64(args, world, rank, dev, T)
     elif args.workload == "sweep":
         res = run_sweep(args, world, rank, dev, T)
     else:

@@ -162,6 +162,33 @@ def gen_c3(nblocks, seed, dev, first_block=0, carry_fn=None, start0=0):
     return vals, starts
 
 
+def gen_c3_64(nunits, seed, dev, first_block=0, carry_fn=None, start0=(1 << 40) + 12345):
+    """The C3 posting list as 64-bit ids (p4D1Enc256v64 units of 256): the
+    same gaps as gen_c3, values start0 + sum of gaps 0..e (no 2^32 wrap; the
+    default start0 puts every id above 2^32).  Returns (values [nunits,256]
+    int64, per-unit starts [nunits] int64: the value preceding each unit)."""
+    n = nunits * 256
+    e0 = first_block * 256
+    vals = torch.empty(n, dtype=torch.int64, device=dev)
+    run = 0
+    for a in range(0, n, CHUNK):
+        m = min(CHUNK, n - a)
+        vals[a:a + m] = torch.cumsum(c3_gaps(e0 + a, m, seed, dev), 0) + run
+        run = int(vals[a + m - 1].item())
+    if carry_fn is None:
+        assert first_block == 0, "a shard past unit 0 needs the carry of the earlier shards"
+        before = 0
+    else:
+        before = int(carry_fn(run))
+    base = start0 + before
+    vals += base
+    vals = vals.view(nunits, 256)
+    starts = torch.empty(nunits, dtype=torch.int64, device=dev)
+    starts[0] = base
+    starts[1:] = vals[:-1, -1]
+    return vals, starts
+
+
 def gen_c1(nblocks, n, seed, dev, first_block=0):
     """configs[0]: n-value blocks uniform in [0, 255] (ab_test.cpp:1610-1631)."""
     vals = torch.empty(nblocks * n, dtype=torch.int32, device=dev)

@@ -91,6 +91,32 @@ int tpf_p4d1dec256v32_chain_sums(const uint8_t *d_in, uint64_t in_bytes, const u
 int tpf_p4d1dec256v32_chain_decode(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks,
                                    uint32_t *d_out, uint32_t base, const void *d_ws, uint64_t *d_err, void *stream);
 
+/* ---- 64-bit chained delta-1 decode (128v64 / 256v64) --------------------
+ * The 64-bit counterpart of the chained 256v32 decode: nunits consecutive
+ * p4D1Enc256v64 (fmt TPF_FMT_256V64, 256 values per unit) or p4D1Enc128v64
+ * (TPF_FMT_128V64, 128) units chained the way reference callers chain them
+ * (start of unit i = last value of unit i-1, README.md:116-123; reference
+ * decoder p4d1dec256v64_scalar.cpp:15-32, which carries the start across its
+ * two 128-value blocks the same way).  Phase A (chain_sums) decodes every
+ * unit's delta total sum(v + 1) mod 2^64 and prefix-sums them into the
+ * workspace; phase B (chain_decode) decodes with start(i) = base + the totals
+ * before i.  tpf_d1dec64_chained = A + B with base = start0; for a sharded list
+ * exchange the d_total of each shard (one u64) as for 256v32.  d_out: nunits *
+ * 128 * (1 or 2) u64. */
+size_t tpf_d1dec64_chain_workspace_size(uint64_t nunits);
+int tpf_d1dec64_chained(int fmt, const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nunits,
+                        uint64_t *d_out, uint64_t start0, void *d_ws, size_t ws_bytes, uint64_t *d_err, void *stream);
+int tpf_d1dec64_chain_sums(int fmt, const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nunits,
+                           void *d_ws, size_t ws_bytes, uint64_t *d_total, uint64_t *d_err, void *stream);
+int tpf_d1dec64_chain_decode(int fmt, const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nunits,
+                             uint64_t *d_out, uint64_t base, const void *d_ws, uint64_t *d_err, void *stream);
+/* Named forms: replace a caller's loop of turbopfor::p4D1Dec256v64 /
+ * p4D1Dec128v64 calls (include/turbopfor.h:80,67) over one chained list. */
+int tpf_p4d1dec256v64_chained(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nunits,
+                              uint64_t *d_out, uint64_t start0, void *d_ws, size_t ws_bytes, uint64_t *d_err, void *stream);
+int tpf_p4d1dec128v64_chained(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nunits,
+                              uint64_t *d_out, uint64_t start0, void *d_ws, size_t ws_bytes, uint64_t *d_err, void *stream);
+
 /* ---- 256v32 encode ---------------------------------------------------
  * Replaces turbopfor::p4Enc256v32 (include/turbopfor.h:33, dispatch.cpp:70-77)
  * and p4D1Enc256v32 (:36, dispatch.cpp:79-86) for nblocks blocks of 256

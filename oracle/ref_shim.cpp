@@ -192,6 +192,75 @@ double tpref_d1dec256v32_stream_mt(const uint8_t * in, const uint64_t * off, con
     return std::chrono::duration<double>(t1 - t0).count();
 }
 
+// The 64-bit posting-list reader: p4D1Dec256v64 over nunits consecutive
+// 256v64 units, each thread a contiguous range; chained != 0 takes starts[]
+// only for a thread's first unit and carries the previous unit's last value
+// (README.md:116-123).  Returns wall seconds of the parallel region.
+double tpref_d1dec256v64_stream_mt(const uint8_t * in, const uint64_t * off, const uint64_t * starts, uint64_t nunits, uint64_t * out,
+                                   int nthreads, int use_dispatch, int chained)
+{
+    if (nthreads < 1)
+        nthreads = 1;
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t)
+    {
+        uint64_t lo = nunits * (uint64_t)t / (uint64_t)nthreads;
+        uint64_t hi = nunits * (uint64_t)(t + 1) / (uint64_t)nthreads;
+        th.emplace_back([=] {
+            for (uint64_t i = lo; i < hi; ++i)
+            {
+                uint64_t * o = out + i * 256u;
+                const uint64_t st = (chained && i > lo) ? o[-1] : starts[i];
+                if (use_dispatch)
+                    turbopfor::p4D1Dec256v64(in + off[i], 256u, o, st);
+                else
+                    turbopfor::scalar::p4D1Dec256v64(in + off[i], 256u, o, st);
+            }
+        });
+    }
+    for (auto & x : th)
+        x.join();
+    auto t1 = std::chrono::steady_clock::now();
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// The posting-list writer: p4D1Enc256v32 over nblocks blocks of one list,
+// each thread a contiguous range chained through the returned end pointers
+// into its own slice of `scratch` (range x `slot` bytes), block i started
+// from starts[i] for a thread's first block and from the previous block's
+// last input value after that (README.md:108-123).  off[i] = block i's
+// offset in scratch.  Returns wall seconds, or -1 on a bad slot.
+double tpref_d1enc256v32_stream_mt(const uint32_t * vals, const uint32_t * starts, uint64_t nblocks, uint8_t * scratch, uint64_t slot,
+                                   uint64_t * off, int nthreads, int use_dispatch)
+{
+    if (nthreads < 1)
+        nthreads = 1;
+    if (slot < 1040)
+        return -1.0;
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t)
+    {
+        uint64_t lo = nblocks * (uint64_t)t / (uint64_t)nthreads;
+        uint64_t hi = nblocks * (uint64_t)(t + 1) / (uint64_t)nthreads;
+        th.emplace_back([=] {
+            uint8_t * e = scratch + lo * slot;
+            for (uint64_t i = lo; i < hi; ++i)
+            {
+                off[i] = static_cast<uint64_t>(e - scratch);
+                uint32_t * in = const_cast<uint32_t *>(vals + i * 256u);
+                const uint32_t st = i > lo ? vals[i * 256u - 1u] : starts[i];
+                e = use_dispatch ? turbopfor::p4D1Enc256v32(in, 256u, e, st) : turbopfor::scalar::p4D1Enc256v32(in, 256u, e, st);
+            }
+        });
+    }
+    for (auto & x : th)
+        x.join();
+    auto t1 = std::chrono::steady_clock::now();
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
 // Round trip of nblocks blocks of 256 u32 (block i at vals + 256 i): each
 // thread encodes its contiguous range with p4Enc256v32, chaining through the
 // returned end pointers into its own slice of `scratch` (slice = range x

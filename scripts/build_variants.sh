@@ -9,6 +9,7 @@ HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 FLAGS="--offload-arch=gfx950 -O3 -std=c++20 -shared -fPIC -munsafe-fp-atomics -I turbopfor-cpp_amd/csrc -I include"
 make -s -C turbopfor-cpp_amd
 $HIPCC $FLAGS -o scripts/libdecvar.so scripts/dec_variants.hip &
+$HIPCC $FLAGS -o scripts/libdecgrp.so scripts/dec_groups.hip &
 $HIPCC $FLAGS -o scripts/libencvar.so scripts/enc_variants.hip -L turbopfor-cpp_amd/lib -lturbopfor_amd \
     -Wl,-rpath,'$ORIGIN/../turbopfor-cpp_amd/lib'
 wait

@@ -20,11 +20,21 @@ def _dec(mode):
     return lambda n: "k_dec256v32w" in n and (f"StartModeE{mode}E" in n or f"StartMode){mode}," in n)
 
 
+def _dec64(nb, mode):
+    """k_dec128v64w<nb, Start64 mode> (mangled or demangled)."""
+    return lambda n: "k_dec128v64w" in n and (f"ILj{nb}ELNS0_7Start64E{mode}E" in n or f"<{nb}u, (tpf::dev::Start64){mode}>" in n)
+
+
+def _enc32(kind, d1):
+    return lambda n: f"k_enc256v32_{kind}" in n and (f"ILb{int(d1)}E" in n or f"<{'true' if d1 else 'false'}" in n)
+
+
 # workload -> (kernel name tests, description): one test per kernel of the
 # step; a step's traffic is the sum of each kernel's per-launch median.
 # Names appear demangled or mangled.
 KERNELS = {
     "c2": ([_dec(0)], "tpf::dev::k_dec256v32w<StartMode::None>"),
+    "c5": ([_dec(0)], "tpf::dev::k_dec256v32w<StartMode::None> (C5 shard: bw 8 / bw 16)"),
     "c3": ([_dec(1)], "tpf::dev::k_dec256v32w<StartMode::PerBlock>"),
     "c1": ([lambda n: "k_dec_h32w" in n], "tpf::dev::k_dec_h32w (windowed p4Dec32 batch)"),
     # chained list: phase A (block sums) + phase B (prefix decode); the run
@@ -32,14 +42,17 @@ KERNELS = {
     "c3chain": ([lambda n: "k_dsum256v32_lanes" in n, _dec(2)], "k_dsum256v32_lanes (phase A) + k_dec256v32w<Prefix>"),
     # round trip: encoder plan + write passes (non-D1) + decode; the run
     # scan between the passes (625K run totals, ~7.5 MB) is not counted
-    "c4": ([lambda n: "k_enc256v32_plan" in n and ("ILb0E" in n or "<false" in n),
-            lambda n: "k_enc256v32_write" in n and ("ILb0E" in n or "<false" in n), _dec(0)],
+    "c4": ([_enc32("plan", False), _enc32("write", False), _dec(0)],
            "k_enc256v32_plan<false> + k_enc256v32_write<false> + k_dec256v32w<StartMode::None>"),
     # C4's 64-bit leg (same rocprof runs as c4): 256v64 encode passes + decode
     "c4_64": ([lambda n: "k_enc128v64_plan" in n and ("ILj2ELb0E" in n or "<2u, false" in n),
                lambda n: "k_enc128v64_write" in n and ("ILj2ELb0E" in n or "<2u, false" in n),
-               lambda n: "k_dec128v64w" in n and ("ILj2ELb0E" in n or "<2u, false" in n)],
-              "k_enc128v64_plan<2,false> + k_enc128v64_write<2,false> + k_dec128v64w<2,false>"),
+               _dec64(2, 0)],
+              "k_enc128v64_plan<2,false> + k_enc128v64_write<2,false> + k_dec128v64w<2,None>"),
+    # D1 encode of the C3 posting list: plan + write passes (run scan not counted)
+    "c3enc": ([_enc32("plan", True), _enc32("write", True)], "k_enc256v32_plan<true> + k_enc256v32_write<true>"),
+    # 64-bit chained list: phase A (unit sums) + phase B (prefix decode)
+    "c3chain64": ([_dec64(2, 3), _dec64(2, 2)], "k_dec128v64w<2,Sum> (phase A) + k_dec128v64w<2,Prefix>"),
 }
 
 

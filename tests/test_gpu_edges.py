@@ -210,3 +210,48 @@ def test_run_scan_matches_cumsum(nruns):
     got = d_base.cpu().numpy().view(np.uint64)[:nruns]
     assert np.array_equal(got, excl)
     assert int(d_total.cpu().numpy().view(np.uint64)[0]) == (int(incl[-1]) if nruns else 0)
+
+
+def test_out_of_format_widths_reported():
+    """a block whose width field is outside its format (32-bit: b or
+    bx > 32; p4Dec32 constant: b > 32) is rejected by the host framing
+    (tpf_scan_offsets) AND reported by every device decoder through d_err,
+    even when the caller's offsets match the clamped parse; the blocks before
+    it decode exactly."""
+    import oracle_lib
+
+    L = tpf.lib()
+    rng = np.random.default_rng(8)
+    good = rng.integers(0, 1 << 9, size=(5, 256), dtype=np.uint64).astype(np.uint32)
+    gp, go = oracle_lib.enc256v32_batch(good)
+    bad_blocks = [bytes([0x21]) + bytes(32 * 32),              # plain, b = 33 (clamped parse: 1025 B)
+                  bytes([0x85, 40]) + bytes(32) + bytes(32 * 5),  # bitmap, bx = 40, no exceptions
+                  bytes([0x40 | 33, 1]) + bytes(32 * 32) + bytes([7, 3])]  # vbyte, b = 33
+    for k, blk in enumerate(bad_blocks):
+        stream = np.concatenate([gp, np.frombuffer(blk, np.uint8), gp[: go[1]]])
+        offs = np.concatenate([go, [go[-1] + len(blk), go[-1] + len(blk) + go[1]]]).astype(np.int64)
+        nb = len(offs) - 1
+        L.tpf_scan_offsets.restype = ctypes.c_int64
+        scanned = np.zeros(nb + 1, dtype=np.uint64)
+        assert L.tpf_scan_offsets(2, ctypes.c_void_p(stream.ctypes.data), ctypes.c_uint64(len(stream)), 256, ctypes.c_uint64(nb),
+                                  ctypes.c_void_p(scanned.ctypes.data)) < 0, k
+        err = torch.zeros(1, dtype=torch.int64, device=DEV)
+        out = tpf.dec256v32(torch.from_numpy(stream).to(DEV), torch.from_numpy(offs).to(DEV), nb, err=err)
+        torch.cuda.synchronize()
+        assert int(err.item()) == 5, k
+        np.testing.assert_array_equal(out[:5].cpu().numpy().view(np.uint32), good)
+        err.zero_()
+        out = tpf.dec_batch("256v32", torch.from_numpy(stream).to(DEV), torch.from_numpy(offs).to(DEV), nb, 200, err=err)
+        torch.cuda.synchronize()
+        assert int(err.item()) == 5, ("generic", k)
+    # p4Dec32 constant block wider than 32 bits: 1 + 5 bytes by the clamped parse
+    g32 = rng.integers(0, 200, size=(3, 127), dtype=np.uint64).astype(np.uint32)
+    p32, o32 = oracle_lib.enc32_batch(g32)
+    blk = bytes([0xC0 | 40]) + bytes(5)
+    stream = np.concatenate([p32, np.frombuffer(blk, np.uint8)])
+    offs = np.concatenate([o32, [o32[-1] + len(blk)]]).astype(np.int64)
+    err = torch.zeros(1, dtype=torch.int64, device=DEV)
+    out = tpf.dec_batch("32", torch.from_numpy(stream).to(DEV), torch.from_numpy(offs).to(DEV), 4, 127, err=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 3
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32).reshape(4, 127)[:3], g32)

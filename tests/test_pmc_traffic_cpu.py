@@ -70,9 +70,25 @@ def test_round3_kernels(tmp_path):
     assert d["hbm_bytes_per_launch"] == (2 * 4 + 9) * 1024
     p64 = "void tpf::dev::k_enc128v64_plan<2u, false>(unsigned long const*, unsigned long)"
     w64 = "void tpf::dev::k_enc128v64_write<2u, false>(unsigned long const*, unsigned long)"
-    d64 = "void tpf::dev::k_dec128v64w<2u, false>(unsigned char const*, unsigned long)"
+    d64 = "void tpf::dev::k_dec128v64w<2u, (tpf::dev::Start64)0>(tpf::dev::Dec64Args)"
     d = _run(tmp_path, "c4_64", [(p64, 1), (w64, 2), (d64, 3), (PLAN, 100)], [(p64, 0), (w64, 5), (d64, 6), (PLAN, 100)], out)
     assert d["FETCH_SIZE_KiB_median"] == 6 and d["WRITE_SIZE_KiB_median"] == 11
+
+
+def test_round4_kernels(tmp_path):
+    """c3enc = the D1 encoder's two passes; c3chain64 = the 64-bit chained
+    decode's Sum and Prefix launches (mangled names, as rocprofv3 may print)."""
+    out = tmp_path / "t.json"
+    pl1 = "_ZN3tpf3dev16k_enc256v32_planILb1ELi0EEEvPKjm"
+    wr1 = "_ZN3tpf3dev17k_enc256v32_writeILb1ELi0EEEvPKjm"
+    pl0 = "_ZN3tpf3dev16k_enc256v32_planILb0ELi0EEEvPKjm"
+    d = _run(tmp_path, "c3enc", [(pl1, 3), (wr1, 4), (pl0, 99)], [(pl1, 0), (wr1, 7), (pl0, 99)], out)
+    assert d["FETCH_SIZE_KiB_median"] == 7 and d["WRITE_SIZE_KiB_median"] == 7
+    s3 = "_ZN3tpf3dev12k_dec128v64wILj2ELNS0_7Start64E3EEEvNS0_9Dec64ArgsE"
+    s2 = "_ZN3tpf3dev12k_dec128v64wILj2ELNS0_7Start64E2EEEvNS0_9Dec64ArgsE"
+    s1 = "_ZN3tpf3dev12k_dec128v64wILj2ELNS0_7Start64E1EEEvNS0_9Dec64ArgsE"
+    d = _run(tmp_path, "c3chain64", [(s3, 10), (s2, 20), (s1, 500)], [(s3, 0), (s2, 40), (s1, 500)], out)
+    assert d["FETCH_SIZE_KiB_median"] == 30 and d["WRITE_SIZE_KiB_median"] == 40
 
 
 def test_committed_traffic_matches_these_kernels():

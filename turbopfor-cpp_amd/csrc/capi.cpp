@@ -191,6 +191,70 @@ int tpf_p4d1dec256v32_chained(const uint8_t * d_in, uint64_t in_bytes, const uin
     return tpf_p4d1dec256v32_chain_decode(d_in, in_bytes, d_off, nblocks, d_out, start0, d_ws, nullptr, stream);
 }
 
+// ---- 64-bit chained delta-1 decode (128v64 / 256v64 units) ----------------
+static int chain64_nb(int fmt) { return fmt == TPF_FMT_256V64 ? 2 : fmt == TPF_FMT_128V64 ? 1 : 0; }
+
+size_t tpf_d1dec64_chain_workspace_size(uint64_t nunits) { return tpf::d1chain64_workspace(nunits); }
+
+int tpf_d1dec64_chain_sums(int fmt, const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nunits, void * d_ws,
+                           size_t ws_bytes, uint64_t * d_total, uint64_t * d_err, void * stream)
+{
+    if (int rc = check_device())
+        return rc;
+    const int nb = chain64_nb(fmt);
+    if (!nb)
+        return fail(TPF_EINVAL, "tpf_d1dec64_chain_sums: fmt must be TPF_FMT_128V64 or TPF_FMT_256V64");
+    if (nunits && (!d_in || !d_off || !d_ws))
+        return fail(TPF_EINVAL, "tpf_d1dec64_chain_sums: null pointer");
+    if (ws_bytes < tpf_d1dec64_chain_workspace_size(nunits))
+        return fail(TPF_EINVAL, "tpf_d1dec64_chain_sums: workspace too small");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (int rc = prep_err(d_err, s))
+        return rc;
+    hipError_t e = tpf::launch_d1chain64_sums(static_cast<uint32_t>(nb), d_in, in_bytes, d_off, nunits, d_ws, ws_bytes, d_total,
+                                              reinterpret_cast<unsigned long long *>(d_err), s);
+    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_d1dec64_chain_sums");
+}
+
+int tpf_d1dec64_chain_decode(int fmt, const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nunits, uint64_t * d_out,
+                             uint64_t base, const void * d_ws, uint64_t * d_err, void * stream)
+{
+    if (int rc = check_device())
+        return rc;
+    const int nb = chain64_nb(fmt);
+    if (!nb)
+        return fail(TPF_EINVAL, "tpf_d1dec64_chain_decode: fmt must be TPF_FMT_128V64 or TPF_FMT_256V64");
+    if (nunits && (!d_in || !d_off || !d_out || !d_ws))
+        return fail(TPF_EINVAL, "tpf_d1dec64_chain_decode: null pointer");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (int rc = prep_err(d_err, s))
+        return rc;
+    hipError_t e = tpf::launch_d1chain64_decode(static_cast<uint32_t>(nb), d_in, in_bytes, d_off, nunits, d_out, d_ws, base,
+                                                reinterpret_cast<unsigned long long *>(d_err), s);
+    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_d1dec64_chain_decode");
+}
+
+int tpf_d1dec64_chained(int fmt, const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nunits, uint64_t * d_out,
+                        uint64_t start0, void * d_ws, size_t ws_bytes, uint64_t * d_err, void * stream)
+{
+    if (int rc = tpf_d1dec64_chain_sums(fmt, d_in, in_bytes, d_off, nunits, d_ws, ws_bytes, nullptr, d_err, stream))
+        return rc;
+    // phase B re-checks lengths; keep the first error index from phase A
+    return tpf_d1dec64_chain_decode(fmt, d_in, in_bytes, d_off, nunits, d_out, start0, d_ws, nullptr, stream);
+}
+
+int tpf_p4d1dec256v64_chained(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nunits, uint64_t * d_out,
+                              uint64_t start0, void * d_ws, size_t ws_bytes, uint64_t * d_err, void * stream)
+{
+    return tpf_d1dec64_chained(TPF_FMT_256V64, d_in, in_bytes, d_off, nunits, d_out, start0, d_ws, ws_bytes, d_err, stream);
+}
+
+int tpf_p4d1dec128v64_chained(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nunits, uint64_t * d_out,
+                              uint64_t start0, void * d_ws, size_t ws_bytes, uint64_t * d_err, void * stream)
+{
+    return tpf_d1dec64_chained(TPF_FMT_128V64, d_in, in_bytes, d_off, nunits, d_out, start0, d_ws, ws_bytes, d_err, stream);
+}
+
 uint64_t tpf_p4enc256v32_bound(uint64_t nblocks) { return nblocks * 1800u + 64u; }
 
 size_t tpf_p4enc256v32_workspace_size(uint64_t nblocks) { return tpf::enc256v32_workspace(nblocks); }

@@ -232,19 +232,21 @@ __device__ __forceinline__ uint32_t decode_block256v32(const uint32_t * lds, uin
         const uint32_t hdr = (h & 0x80u) ? 2u : 1u;
         const uint32_t bx = (h & 0x80u) ? min(x1, 32u) : 0u;
         const uint32_t b = min(h & 0x7Fu, 32u);
+        const uint32_t bad = ((h & 0x7Fu) > 32u || ((h & 0x80u) && x1 > 32u)) ? kWidthBad : 0u;
         if (bx == 0u)
         {
             v = unpack256v32_lane(lds, s + hdr, b, t);
-            return hdr + 32u * b;
+            return (hdr + 32u * b) | bad;
         }
         const BitmapInfo bi = read_bitmap256(wbm, t);
         const uint32_t xs = s + 34u;
         const uint32_t xbytes = (bi.xn * bx + 7u) >> 3;
         v = unpack256v32_lane(lds, xs + xbytes, b, t);
         patch_bitmap256(lds, bi, xs, bx, b, t, v);
-        return 34u + xbytes + 32u * b;
+        return (34u + xbytes + 32u * b) | bad;
     }
     const uint32_t b = min(h & 0x3Fu, 32u);
+    const uint32_t bad = (h & 0x3Fu) > 32u ? kWidthBad : 0u;
     const uint32_t xn = x1;
     v = unpack256v32_lane(lds, s + 2u, b, t);
     const uint32_t end = vbyte_exceptions(lds, s + 2u + 32u * b, xn, scr, t);
@@ -253,7 +255,7 @@ __device__ __forceinline__ uint32_t decode_block256v32(const uint32_t * lds, uin
     v.y |= shl32(ex.y, b);
     v.z |= shl32(ex.z, b);
     v.w |= shl32(ex.w, b);
-    return end - s;
+    return (end - s) | bad;
 }
 
 // Delta-1 (applyDelta1_256, p4d1dec256v32_scalar.cpp:39-50): inclusive scan

@@ -224,6 +224,15 @@ __device__ __forceinline__ bool dsum_pass(const DecArgs & A, const DsumRun & R, 
     return true;
 }
 
+// Last LDS byte position dsum_lanes may clamp to: its widest read is 9
+// dwords from a clamped position (base_sum_lanes, the raw-vbyte loop), and
+// the wave's window holds (WB + 64) / 4 dwords, so clamped reads stay inside
+// the wave's own window (WB + 40 let them run 3 dwords into the
+// next wave's).  Valid blocks lie inside [0, WB) and never reach the clamp.
+template <uint32_t WB>
+constexpr uint32_t kDsumLim = WB + 28u;
+static_assert(kDsumLim<16384u> / 4u + 9u <= (16384u + 64u) / 4u, "clamped phase-A reads stay in the wave's window");
+
 #ifndef TPF_DSUM_WAVES
 #define TPF_DSUM_WAVES 2
 #endif
@@ -320,7 +329,7 @@ __global__ __launch_bounds__(256, TPF_DSUM_WAVES) void k_dsum256v32_lanes(const 
 #ifdef TPF_DSUM_STAGEONLY // measurement builds only (scripts/chain_phase_probe.py)
         const bool ok = true;
 #else
-        const bool ok = dsum_lanes<WB + 40u>(win, p, cur.len, in_win, tab, s);
+        const bool ok = dsum_lanes<kDsumLim<WB>>(win, p, cur.len, in_win, tab, s);
 #endif
         sumv = in_win ? s : sumv;
         cur.fb = cur.fb || (in_win && !ok);

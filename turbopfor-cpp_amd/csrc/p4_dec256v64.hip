@@ -17,6 +17,7 @@
 // Header b = 63 means 64 (p4_scalar_internal.cpp:645-649).
 #include "p4_dec_run.h"
 #include "p4_generic.h"
+#include "p4_scan.h"
 #include "tpf_kernels.h"
 
 namespace tpf::dev
@@ -72,11 +73,12 @@ __device__ __forceinline__ uint32_t decode_block128v64(const uint32_t * lds, uin
         uint32_t b = h & 0x7Fu;
         if (b == 63u)
             b = 64u;
+        const uint32_t bad = (b > 64u || ((h & 0x80u) && x1b > 64u)) ? kWidthBad : 0u;
         b = min(b, 64u);
         if (bx == 0u)
         {
             unpack128v64_lane(lds, s + hdr, b, t, x0, x1);
-            return hdr + 16u * b;
+            return (hdr + 16u * b) | bad;
         }
         // 128-bit bitmap at s+2: lane t's bits 2t, 2t+1 sit in dword t>>4;
         // rank = popcount of the dwords before (lanes 0,16,32,48 each bring
@@ -95,7 +97,7 @@ __device__ __forceinline__ uint32_t decode_block128v64(const uint32_t * lds, uin
         const uint64_t ex1 = lds_bits64(lds, xs * 8u + (before + (my & 1u)) * bx, bx);
         x0 |= (my & 1u) ? shl64(ex0, b) : 0ull;
         x1 |= (my & 2u) ? shl64(ex1, b) : 0ull;
-        return 18u + xbytes + 16u * b;
+        return (18u + xbytes + 16u * b) | bad;
     }
     uint32_t b = h & 0x3Fu;
     if (b == 63u)
@@ -119,17 +121,54 @@ __device__ __forceinline__ uint64_t delta1_128v64(uint64_t & x0, uint64_t & x1, 
     return start + readlane_u64(incl, 63);
 }
 
+// Start handling of a run (the 32-bit decoder's StartMode, p4_dec256v32.hip):
+//   None    p4Dec128v64 / p4Dec256v64
+//   PerUnit p4D1Dec*v64 with the start of unit i = starts[i]
+//   Prefix  one chained list (round 4): start of unit i = base + the unit sums
+//           before it (phase A below + the run scan, p4_scan.h), so a chained
+//           list decodes with only its initial start
+//   Sum     phase A of the chained decode: each unit's delta total
+//           sum(v + 1) mod 2^64 (decoded, not stored) and one total per run
+enum class Start64 : int
+{
+    None = 0,
+    PerUnit = 1,
+    Prefix = 2,
+    Sum = 3,
+};
+
+struct Dec64Args
+{
+    const uint8_t * in;
+    uint64_t in_bytes;
+    const uint64_t * off;
+    uint64_t nunits;
+    uint64_t * out;
+    const uint64_t * starts;          // PerUnit: starts; Prefix: phase A's unit sums
+    uint64_t base;                    // Prefix: the value preceding unit 0
+    uint64_t * sums;                  // Sum: unit sums
+    uint64_t * run_tot;               // Sum: one total per run
+    const uint64_t * run_pre;         // Prefix: run scan
+    const uint64_t * run_tile;        // Prefix: run scan
+    unsigned long long * err;
+};
+
+constexpr uint32_t kRun64 = 16; // units per wave run (both phases: a Prefix run is a Sum run)
+
 // output store policy (A/B knob): 0 = nt, 1 = sc1 nt through a run descriptor
 #ifndef TPF_D64_SC1NT
 #define TPF_D64_SC1NT 0
 #endif
-template <uint32_t NB, bool D1>
-__global__ __launch_bounds__(256, 4) void k_dec128v64w(const uint8_t * __restrict in, uint64_t in_bytes,
-                                                       const uint64_t * __restrict off, uint64_t nunits,
-                                                       uint64_t * __restrict out, const uint64_t * __restrict starts,
-                                                       unsigned long long * __restrict err)
+template <uint32_t NB, Start64 SM>
+__global__ __launch_bounds__(256, 4) void k_dec128v64w(const Dec64Args A)
 {
-    constexpr uint32_t kRun = 16, NC = 3;
+    constexpr uint32_t kRun = kRun64, NC = 3;
+    constexpr bool D1 = SM == Start64::PerUnit || SM == Start64::Prefix;
+    const uint8_t * in = A.in;
+    const uint64_t in_bytes = A.in_bytes, nunits = A.nunits;
+    const uint64_t * off = A.off;
+    uint64_t * out = A.out;
+    unsigned long long * err = A.err;
     __shared__ uint32_t slots[4][kSlot64 / 4];
     __shared__ uint64_t scratch[4][512];
     const uint32_t t = threadIdx.x & 63u;
@@ -148,7 +187,16 @@ __global__ __launch_bounds__(256, 4) void k_dec128v64w(const uint8_t * __restric
     const uint64_t e = valid ? off[unit + 1u] : 0ull;
     RunPlaneT<kSlot64> P;
     P.init(in_base, in_base + in_bytes, o, e, valid);
-    const uint64_t startv = (D1 && valid) ? starts[unit] : 0ull;
+    uint64_t startv = 0ull;
+    if constexpr (SM == Start64::PerUnit)
+        startv = valid ? A.starts[unit] : 0ull;
+    if constexpr (SM == Start64::Prefix)
+    {
+        // lane t: base + the run's base + the sums of the run's units before first+t
+        const uint64_t sv = valid ? A.starts[unit] : 0ull;
+        startv = A.base + run_base(A.run_pre, A.run_tile, first / kRun) + (wave_incl_scan64(sv) - sv);
+    }
+    uint64_t sumv = 0ull; // Sum: lane jj = unit first+jj's delta total
     UsedLanes usedv;
     uint64_t * const out_run = out + first * (128u * NB);
 #if TPF_D64_SC1NT
@@ -160,11 +208,21 @@ __global__ __launch_bounds__(256, 4) void k_dec128v64w(const uint8_t * __restric
         uint32_t s = (ctl >> kCtlShift) & 15u;
         const uint32_t s0 = s;
         uint64_t carry = D1 ? readlane_u64(startv, jj) : 0ull;
+        uint64_t usum = 0ull;
+        uint32_t wbad = 0u;
 #pragma unroll
         for (uint32_t u = 0; u < NB; ++u)
         {
             uint64_t x0, x1;
-            s += decode_block128v64(slot, s, scr, t, x0, x1);
+            const uint32_t used = decode_block128v64(slot, s, scr, t, x0, x1);
+            s += used & ~kWidthBad; // a flagged first block: the second is still parsed in the slot
+            wbad |= used & kWidthBad;
+            if constexpr (SM == Start64::Sum)
+            {
+                usum += readlane_u64(wave_incl_scan64(x0 + x1 + 2ull), 63);
+                wave_lds_sync();
+                continue;
+            }
             if constexpr (D1)
                 carry = delta1_128v64(x0, x1, carry);
 #if TPF_D64_SC1NT
@@ -177,7 +235,9 @@ __global__ __launch_bounds__(256, 4) void k_dec128v64w(const uint8_t * __restric
 #endif
             wave_lds_sync();
         }
-        usedv.put(s - s0, jj, t);
+        usedv.put((s - s0) | wbad, jj, t);
+        if constexpr (SM == Start64::Sum)
+            sumv = t == jj ? usum : sumv;
     };
 
     Chunk C[NC];
@@ -198,6 +258,14 @@ __global__ __launch_bounds__(256, 4) void k_dec128v64w(const uint8_t * __restric
             }
         }
     }
+    if constexpr (SM == Start64::Sum)
+    {
+        if (valid)
+            A.sums[unit] = sumv;
+        const uint64_t rt = readlane_u64(wave_incl_scan64(valid ? sumv : 0ull), 63);
+        if (t == 0)
+            A.run_tot[first / kRun] = rt;
+    }
     const uint64_t badmask = usedv.bad(P.len, valid);
     if (err != nullptr && t == 0 && badmask != 0u)
         atomicMin(err, static_cast<unsigned long long>(first + __builtin_ctzll(badmask)));
@@ -208,28 +276,90 @@ __global__ __launch_bounds__(256, 4) void k_dec128v64w(const uint8_t * __restric
 namespace tpf
 {
 
+namespace
+{
+template <dev::Start64 SM>
+hipError_t launch64(uint32_t nb, const dev::Dec64Args & A, hipStream_t s)
+{
+    const uint32_t grid = static_cast<uint32_t>((A.nunits + 4u * dev::kRun64 - 1u) / (4u * dev::kRun64));
+    if (nb == 2u)
+        hipLaunchKernelGGL((dev::k_dec128v64w<2, SM>), dim3(grid), dim3(256), 0, s, A);
+    else
+        hipLaunchKernelGGL((dev::k_dec128v64w<1, SM>), dim3(grid), dim3(256), 0, s, A);
+    return hipGetLastError();
+}
+
+uint64_t runs64(uint64_t nunits) { return (nunits + dev::kRun64 - 1u) / dev::kRun64; }
+size_t al256(size_t x) { return (x + 255u) & ~size_t(255); }
+
+// workspace of the chained decode: unit sums (u64), then the run scan over
+// u64 run totals: totals, in-tile prefixes, tile totals
+struct Chain64Ws
+{
+    uint64_t * sums, * tot, * pre, * tile;
+    static size_t bytes(uint64_t nunits)
+    {
+        const uint64_t r = runs64(nunits);
+        return al256(8u * nunits) + al256(8u * r) + al256(8u * r) + al256(8u * RunScanWs<uint64_t>::tiles(r)) + 256u;
+    }
+    static Chain64Ws carve(void * ws, uint64_t nunits)
+    {
+        const uint64_t r = runs64(nunits);
+        auto * p = static_cast<uint8_t *>(ws);
+        Chain64Ws w;
+        w.sums = reinterpret_cast<uint64_t *>(p);
+        p += al256(8u * nunits);
+        w.tot = reinterpret_cast<uint64_t *>(p);
+        p += al256(8u * r);
+        w.pre = reinterpret_cast<uint64_t *>(p);
+        p += al256(8u * r);
+        w.tile = reinterpret_cast<uint64_t *>(p);
+        return w;
+    }
+};
+} // namespace
+
 // fmt 128v64 (nb = 1) or 256v64 (nb = 2), n == 128 * nb values per unit.
 hipError_t launch_dec128v64(uint32_t nb, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nunits,
                             uint64_t * out, const uint64_t * starts, unsigned long long * err, hipStream_t s)
 {
     if (nunits == 0)
         return hipSuccess;
-    const uint32_t grid = static_cast<uint32_t>((nunits + 63u) / 64u);
-    if (nb == 2u)
-    {
-        if (starts)
-            hipLaunchKernelGGL((dev::k_dec128v64w<2, true>), dim3(grid), dim3(256), 0, s, in, in_bytes, off, nunits, out, starts, err);
-        else
-            hipLaunchKernelGGL((dev::k_dec128v64w<2, false>), dim3(grid), dim3(256), 0, s, in, in_bytes, off, nunits, out, starts, err);
-    }
-    else
-    {
-        if (starts)
-            hipLaunchKernelGGL((dev::k_dec128v64w<1, true>), dim3(grid), dim3(256), 0, s, in, in_bytes, off, nunits, out, starts, err);
-        else
-            hipLaunchKernelGGL((dev::k_dec128v64w<1, false>), dim3(grid), dim3(256), 0, s, in, in_bytes, off, nunits, out, starts, err);
-    }
-    return hipGetLastError();
+    dev::Dec64Args A{in, in_bytes, off, nunits, out, starts, 0ull, nullptr, nullptr, nullptr, nullptr, err};
+    return starts ? launch64<dev::Start64::PerUnit>(nb, A, s) : launch64<dev::Start64::None>(nb, A, s);
+}
+
+// Chained delta-1 decode of a 64-bit list (128v64 / 256v64 units chained the
+// way reference callers chain p4D1Enc256v64, README.md:116-123; inside a
+// 256v64 unit the second block already starts from the first's last value,
+// p4d1dec256v64_scalar.cpp:15-32).  Phase A: every unit's delta total and one
+// total per 16-unit run, then the run scan (u64, mod 2^64); phase B decodes
+// with start(i) = base + the totals before i.
+size_t d1chain64_workspace(uint64_t nunits) { return Chain64Ws::bytes(nunits); }
+
+hipError_t launch_d1chain64_sums(uint32_t nb, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nunits, void * ws,
+                                 size_t ws_bytes, uint64_t * total, unsigned long long * err, hipStream_t s)
+{
+    if (nunits == 0)
+        return total ? hipMemsetAsync(total, 0, 8, s) : hipSuccess;
+    if (ws_bytes < d1chain64_workspace(nunits))
+        return hipErrorInvalidValue;
+    const Chain64Ws w = Chain64Ws::carve(ws, nunits);
+    dev::Dec64Args A{in, in_bytes, off, nunits, nullptr, nullptr, 0ull, w.sums, w.tot, nullptr, nullptr, err};
+    hipError_t e = launch64<dev::Start64::Sum>(nb, A, s);
+    if (e != hipSuccess)
+        return e;
+    return launch_run_scan_u64t(w.tot, runs64(nunits), w.pre, w.tile, total, s);
+}
+
+hipError_t launch_d1chain64_decode(uint32_t nb, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nunits,
+                                   uint64_t * out, const void * ws, uint64_t base, unsigned long long * err, hipStream_t s)
+{
+    if (nunits == 0)
+        return hipSuccess;
+    const Chain64Ws w = Chain64Ws::carve(const_cast<void *>(ws), nunits);
+    dev::Dec64Args A{in, in_bytes, off, nunits, out, w.sums, base, nullptr, nullptr, w.pre, w.tile, err};
+    return launch64<dev::Start64::Prefix>(nb, A, s);
 }
 
 } // namespace tpf

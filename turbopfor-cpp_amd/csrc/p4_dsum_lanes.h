@@ -204,7 +204,8 @@ __device__ __forceinline__ bool dsum_lanes(const uint32_t * w, uint32_t p, uint3
     const bool is_bm = is_pb && bx != 0u;
     const uint32_t hdr = (h & 0x80u) ? 2u : 1u;
     uint32_t b = is_const ? 0u : is_vb ? min(h & 0x3Fu, 32u) : min(h & 0x7Fu, 32u);
-    bool ok = act;
+    // a width field outside 32 bits: the wave decoder flags it (kWidthBad)
+    bool ok = act && !(is_vb && (h & 0x3Fu) > 32u) && !(is_pb && ((h & 0x7Fu) > 32u || ((h & 0x80u) && x1 > 32u)));
     uint32_t exsum = 0u, xn = is_vb ? x1 : 0u, pay = p + hdr;
 
     // constant block (p4d1dec256v32_scalar.cpp:212-229): 256 * (c + 1)

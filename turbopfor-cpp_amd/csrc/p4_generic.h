@@ -214,6 +214,7 @@ __device__ __forceinline__ uint32_t decode_block_g(const uint32_t * lds, uint32_
         uint32_t b = h & 0x3Fu;
         if (wide && b == 63u)
             b = 64u;
+        const uint32_t cbad = (F == Fmt::H32 && b > 32u) ? kWidthBad : 0u; // framing.cpp: undefined in p4dec32.cpp:100-116
         T c;
         if constexpr (wide)
             c = static_cast<T>(lds_u64(lds, s + 1u) & mask64d(b));
@@ -223,19 +224,21 @@ __device__ __forceinline__ uint32_t decode_block_g(const uint32_t * lds, uint32_
         for (int j = 0; j < 4; ++j)
             v[j] = c;
         *cmode = 1;
-        return 1u + ((b + 7u) >> 3);
+        return (1u + ((b + 7u) >> 3)) | cbad;
     }
-    uint32_t b, bx = 0, hdr, xn = 0, P, xs = 0;
+    uint32_t b, bx = 0, hdr, xn = 0, P, xs = 0, wbad = 0;
     const bool vb = (h & 0x40u) != 0u;
     uint64_t bm[4] = {0, 0, 0, 0};
     uint32_t pc[4] = {0, 0, 0, 0};
     if (!vb)
     {
         hdr = (h & 0x80u) ? 2u : 1u;
-        bx = (h & 0x80u) ? min(uni(lds_byte(lds, s + 1u)), W) : 0u;
+        const uint32_t bxr = (h & 0x80u) ? uni(lds_byte(lds, s + 1u)) : 0u;
+        bx = min(bxr, W);
         b = h & 0x7Fu;
         if (wide && b == 63u)
             b = 64u;
+        wbad = (b > W || bxr > W) ? kWidthBad : 0u;
         b = min(b, W);
         if (bx == 0u)
             P = s + hdr;
@@ -262,6 +265,7 @@ __device__ __forceinline__ uint32_t decode_block_g(const uint32_t * lds, uint32_
         b = h & 0x3Fu;
         if (wide && b == 63u)
             b = 64u;
+        wbad = b > W ? kWidthBad : 0u;
         b = min(b, W);
         xn = uni(lds_byte(lds, s + 1u));
         P = s + 2u;
@@ -276,7 +280,7 @@ __device__ __forceinline__ uint32_t decode_block_g(const uint32_t * lds, uint32_
     if (!vb)
     {
         if (bx == 0u)
-            return hdr + bb;
+            return (hdr + bb) | wbad;
         uint32_t before = 0;
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j)
@@ -292,7 +296,7 @@ __device__ __forceinline__ uint32_t decode_block_g(const uint32_t * lds, uint32_
             }
             before += pc[j];
         }
-        return (xs - s) + pad8d(xn * bx) + bb;
+        return ((xs - s) + pad8d(xn * bx) + bb) | wbad;
     }
     T * tmp = scr + 256;
     const uint32_t end = vbyte_exceptions_g<wide>(lds, P + bb, xn, scr, tmp, t);
@@ -306,7 +310,7 @@ __device__ __forceinline__ uint32_t decode_block_g(const uint32_t * lds, uint32_
         else
             v[j] |= shl32(static_cast<uint32_t>(ex), b);
     }
-    return end - s;
+    return (end - s) | wbad;
 }
 
 // Delta-1 over elements e < n in order (applyDelta1_*): out[e] = start +

@@ -252,7 +252,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
         {
             const uint32_t b = h & 0x3Fu;
             cval = lds_u32(slot, s + 1u) & mask32(b);
-            used = 1u + ((b + 7u) >> 3);
+            used = (1u + ((b + 7u) >> 3)) | (b > 32u ? kWidthBad : 0u);
             pk = (kH32Const << 18);
         }
         else if (h & 0x40u)
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
                 P = s + 2u + pad8d(n) + pad8d(xn * bx);
                 kind = kH32Bitmap;
             }
-            used = (P - s) + pad8d(n * b);
+            used = ((P - s) + pad8d(n * b)) | (((h & 0x7Fu) > 32u || ((h & 0x80u) && ((hw >> 8) & 0xFFu) > 32u)) ? kWidthBad : 0u);
             pk = P | (b << 12) | (kind << 18) | (bx << 20);
         }
         usedv = inw ? used : usedv;

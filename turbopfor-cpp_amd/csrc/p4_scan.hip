@@ -31,8 +31,8 @@ __device__ __forceinline__ bool scan_gated_off(const uint32_t * gate)
     return gate != nullptr && __hip_atomic_load(const_cast<uint32_t *>(gate), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
 }
 
-template <class T>
-__global__ __launch_bounds__(256) void k_run_scan_tiles(const uint32_t * __restrict tot, uint64_t nruns, T * __restrict pre,
+template <class T, class TT>
+__global__ __launch_bounds__(256) void k_run_scan_tiles(const TT * __restrict tot, uint64_t nruns, T * __restrict pre,
                                                          T * __restrict tile, const uint32_t * gate)
 {
     __shared__ T wsum[4];
@@ -114,13 +114,13 @@ namespace tpf
 
 namespace
 {
-template <class T>
-hipError_t run_scan(const uint32_t * tot, uint64_t nruns, T * pre, T * tile, T * total, hipStream_t s, const uint32_t * gate = nullptr)
+template <class T, class TT = uint32_t>
+hipError_t run_scan(const TT * tot, uint64_t nruns, T * pre, T * tile, T * total, hipStream_t s, const uint32_t * gate = nullptr)
 {
     if (nruns == 0)
         return total ? hipMemsetAsync(total, 0, sizeof(T), s) : hipSuccess;
     const uint64_t ntiles = RunScanWs<T>::tiles(nruns);
-    hipLaunchKernelGGL(dev::k_run_scan_tiles<T>, dim3(static_cast<uint32_t>(ntiles)), dim3(256), 0, s, tot, nruns, pre, tile, gate);
+    hipLaunchKernelGGL((dev::k_run_scan_tiles<T, TT>), dim3(static_cast<uint32_t>(ntiles)), dim3(256), 0, s, tot, nruns, pre, tile, gate);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return e;
@@ -133,6 +133,11 @@ hipError_t launch_run_scan_u64(const uint32_t * tot, uint64_t nruns, uint64_t * 
                                const uint32_t * gate)
 {
     return run_scan<uint64_t>(tot, nruns, pre, tile, total, s, gate);
+}
+
+hipError_t launch_run_scan_u64t(const uint64_t * tot, uint64_t nruns, uint64_t * pre, uint64_t * tile, uint64_t * total, hipStream_t s)
+{
+    return run_scan<uint64_t, uint64_t>(tot, nruns, pre, tile, total, s);
 }
 
 hipError_t launch_run_scan_u32(const uint32_t * tot, uint64_t nruns, uint32_t * pre, uint32_t * tile, uint32_t * total, hipStream_t s)

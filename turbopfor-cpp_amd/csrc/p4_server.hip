@@ -122,7 +122,7 @@ __device__ __forceinline__ void srv_serve(SrvLds & L, const ServerReqBox * box, 
         T last = T(0);
         uint32_t used = srv_dec_one<F>(L, 0u, n0, d1, static_cast<T>(start), out, t, &lim, &last);
         uint32_t written = lim;
-        if (pair && n > 128u)
+        if (pair && n > 128u && used < in_len)
         {
             // second 128v64 block, starting after the first one's value 127
             used += srv_dec_one<F>(L, used, n - 128u, d1, last, out + 128, t, &lim, &last);

@@ -60,6 +60,14 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t x, uint32_t l)
     return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
+// OR-ed into a block decoder's consumed-byte count when a width field is
+// outside its format (a 32-bit block with b or bx > 32, a 64-bit one with
+// > 64): the count then disagrees with any offsets, so the batch decoders
+// report the block through d_err exactly as the host framing rejects it
+// (framing.cpp one_block).  Decoders clamp the widths to stay in
+// bounds; the flag keeps the clamped parse from passing for a valid one.
+constexpr uint32_t kWidthBad = 0x80000000u;
+
 __device__ __forceinline__ uint32_t mask32(uint32_t b) { return b >= 32u ? 0xFFFFFFFFu : ((1u << b) - 1u); }
 
 __device__ __forceinline__ uint32_t shl32(uint32_t v, uint32_t b) { return b >= 32u ? 0u : (v << b); }

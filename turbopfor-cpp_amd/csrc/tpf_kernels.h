@@ -75,6 +75,12 @@ hipError_t launch_d1chain_decode(const uint8_t * in, uint64_t in_bytes, const ui
 hipError_t launch_dec128v64(uint32_t nb, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nunits,
                             uint64_t * out, const uint64_t * starts, unsigned long long * err, hipStream_t s);
 
+size_t d1chain64_workspace(uint64_t nunits);
+hipError_t launch_d1chain64_sums(uint32_t nb, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nunits, void * ws,
+                                 size_t ws_bytes, uint64_t * total, unsigned long long * err, hipStream_t s);
+hipError_t launch_d1chain64_decode(uint32_t nb, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nunits,
+                                   uint64_t * out, const void * ws, uint64_t base, unsigned long long * err, hipStream_t s);
+
 size_t enc128v64_workspace(uint64_t nunits);
 hipError_t launch_enc128v64(uint32_t nb, const uint64_t * in, uint64_t nunits, bool d1, const uint64_t * starts, uint64_t start0,
                             uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t s);

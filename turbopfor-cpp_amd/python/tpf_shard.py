@@ -41,6 +41,16 @@ def chained_base(local_total, start0=0, group=None):
     return (start0 + earlier) & 0xFFFFFFFF
 
 
+def chained_base64(local_total, start0=0, group=None):
+    """chained_base for a 64-bit list (tpf_d1dec64_chain_sums totals): this
+    rank's base = start0 + the earlier ranks' totals, mod 2^64."""
+    rank = dist.get_rank(group)
+    t = local_total.to(torch.int64).reshape(1)
+    gathered = [torch.zeros_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(gathered, t, group=group)
+    return (start0 + sum(int(g.item()) & 0xFFFFFFFFFFFFFFFF for g in gathered[:rank])) & 0xFFFFFFFFFFFFFFFF
+
+
 def exclusive_prefix(value, device, group=None):
     """Sum of `value` (a Python int, e.g. a shard's gap total) over the ranks
     before this one: all-gather of one int64 per rank."""

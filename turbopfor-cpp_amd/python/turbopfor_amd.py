@@ -114,7 +114,12 @@ def lib():
         L.tpf_p4ndec256v32_workspace_size.restype = ctypes.c_size_t
         L.tpf_p4ndec256v32.argtypes = [c_vp, c_u64, c_vp, c_u64, ctypes.c_int, ctypes.c_uint32, c_vp, c_vp,
                                        ctypes.c_size_t, c_vp, c_vp]
-        for name in ("tpf_p4nenc256v32", "tpf_p4ndec256v32", "tpf_p4dec256v32_batch", "tpf_p4d1dec256v32_batch", "tpf_p4enc256v32_batch",
+        L.tpf_d1dec64_chain_workspace_size.argtypes = [c_u64]
+        L.tpf_d1dec64_chain_workspace_size.restype = ctypes.c_size_t
+        L.tpf_d1dec64_chained.argtypes = [ctypes.c_int, c_vp, c_u64, c_vp, c_u64, c_vp, c_u64, c_vp, ctypes.c_size_t, c_vp, c_vp]
+        L.tpf_d1dec64_chain_sums.argtypes = [ctypes.c_int, c_vp, c_u64, c_vp, c_u64, c_vp, ctypes.c_size_t, c_vp, c_vp, c_vp]
+        L.tpf_d1dec64_chain_decode.argtypes = [ctypes.c_int, c_vp, c_u64, c_vp, c_u64, c_vp, c_u64, c_vp, c_vp, c_vp]
+        for name in ("tpf_d1dec64_chained", "tpf_d1dec64_chain_sums", "tpf_d1dec64_chain_decode", "tpf_p4nenc256v32", "tpf_p4ndec256v32", "tpf_p4dec256v32_batch", "tpf_p4d1dec256v32_batch", "tpf_p4enc256v32_batch",
                      "tpf_p4d1enc256v32_batch", "tpf_dec_batch", "tpf_enc_batch", "tpf_p4d1dec256v32_chained",
                      "tpf_p4d1dec256v32_chain_sums", "tpf_p4d1dec256v32_chain_decode", "tpf_probe256v32",
                      "tpf_probe_hbm", "tpf_probe_enc256v32"):
@@ -324,6 +329,25 @@ def dec256v32_chained(packed, offsets, nblocks, start0=0, out=None, err=None, ws
     rc = L.tpf_p4d1dec256v32_chained(_ptr(packed), packed.numel(), _ptr(offsets), nblocks, _ptr(out),
                                      ctypes.c_uint32(start0 & 0xFFFFFFFF), _ptr(ws), ws.numel(), _ptr(err),
                                      _stream(torch))
+    _check(rc)
+    return out
+
+
+def dec64_chained(fmt, packed, offsets, nunits, start0=0, out=None, err=None, ws=None):
+    """One chained 64-bit list of fmt "256v64" or "128v64" units (unit i
+    starts from unit i-1's last value, unit 0 from start0): tpf_d1dec64_chained
+    (unit sums + scan, then decode).  Returns int64 [nunits, 256 or 128]."""
+    import torch
+
+    width = _UNIT[fmt]
+    if out is None:
+        out = torch.empty((nunits, width), dtype=torch.int64, device=packed.device)
+    L = lib()
+    ws_bytes = int(L.tpf_d1dec64_chain_workspace_size(nunits))
+    if ws is None or ws.numel() < ws_bytes:
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=packed.device)
+    rc = L.tpf_d1dec64_chained(FMT[fmt], _ptr(packed), packed.numel(), _ptr(offsets), nunits, _ptr(out),
+                               ctypes.c_uint64(start0 & 0xFFFFFFFFFFFFFFFF), _ptr(ws), ws.numel(), _ptr(err), _stream(torch))
     _check(rc)
     return out
 
