@@ -68,8 +68,8 @@ int tpf_perblock_mode(int mode);
  * idles out (10 ms without calls), and HIP's hipDeviceSynchronize, hipFree
  * and hipHostFree wait for every stream of the device: a caller about to do
  * one of those right after per-block calls calls this first to avoid that
- * wait.  tpf_host_dec / tpf_host_enc / tpf_host_release do so themselves and
- * hold other threads' per-block calls back until they return.  Mode 0 needs a large BAR
+ * wait.  The host streams do so themselves around their own allocations and
+ * frees (only there: host streams of different threads run concurrently).  Mode 0 needs a large BAR
  * (VRAM mapped into the CPU's address space); without one the server uses the
  * host-memory mailboxes of mode 2. */
 void tpf_perblock_quiesce(void);
@@ -94,8 +94,9 @@ int64_t tpf_check_offsets(const uint64_t *off, uint64_t nblocks, uint64_t in_byt
  * the work is split into chunks that are copied to HBM, processed and copied
  * back, the upload of chunk k+1 overlapping the kernel and the download of
  * chunk k (a copy stream and a kernel stream).  Host buffers allocated with
- * hipHostMalloc (or registered) give full PCIe rate; pageable buffers are
- * registered (and mapped) for the duration of the call.  Staging buffers and
+ * hipHostMalloc (or registered by the caller) are used as they are (full PCIe
+ * rate); pageable buffers are staged through the pipeline's pinned buffers by
+ * host copies -- the library never page-locks caller memory.  Staging buffers and
  * streams are pooled per device across calls; tpf_host_release() frees them.
  * h_off may be NULL for decode (offsets are scanned with tpf_scan_offsets);
  * given offsets must not decrease and must end at or below in_bytes
@@ -116,6 +117,16 @@ void tpf_host_release(void);
  * repeat a device (two pipelines on one GPU). */
 int tpf_host_dec_multi(const int *devs, int ndev, int fmt, const uint8_t *h_in, uint64_t in_bytes, const uint64_t *h_off,
                        uint64_t nblocks, unsigned n, void *h_vals, const void *h_starts);
+/* Encode one host array on several GPUs at once: the blocks are cut into ndev
+ * contiguous shards of equal block counts and shard d runs tpf_host_enc's
+ * pipeline on device devs[d] from its own thread.  Shard 0 writes straight
+ * into h_out; the others into pooled host staging, moved into place (and
+ * their offsets rebased) once the sizes before them are known.  The bytes
+ * and offsets are identical to tpf_host_enc's (a chained D1 list continues
+ * across shard cuts: each shard starts from the value before its first
+ * block).  Arguments and checks as tpf_host_enc. */
+int tpf_host_enc_multi(const int *devs, int ndev, int fmt, const void *h_vals, uint64_t nblocks, unsigned n, int d1,
+                       const void *h_starts, uint64_t start0, uint8_t *h_out, uint64_t out_cap, uint64_t *h_off);
 
 #ifdef __cplusplus
 }

@@ -102,8 +102,9 @@ def test_reference_style_cpp_caller(tmp_path):
 
 @pytest.mark.parametrize("chunk_bytes", [None, 1000 * 1024, 777 * 1024])
 def test_host_streams_vs_oracle(chunk_bytes, monkeypatch):
-    """Pageable numpy buffers (registered + mapped for the call); with small
-    chunks the pipeline runs many chunks through its 3 slots."""
+    """Pageable numpy buffers (staged through the pipeline's pinned buffers by
+    host copies); with small chunks the pipeline runs many chunks through its
+    3 slots."""
     if chunk_bytes:
         monkeypatch.setenv("TPF_HOST_CHUNK_BYTES", str(chunk_bytes))
     L = capi()
@@ -482,3 +483,42 @@ def test_host_dec_multi_p4dec32():
                               back.ctypes.data, None)
     assert rc == 0, L.tpf_last_error()
     np.testing.assert_array_equal(back, vals)
+
+
+def test_host_enc_multi_vs_single():
+    """tpf_host_enc_multi (SURVEY.md 8 f3 across GPUs, encode side): shards of
+    equal block counts encoded by one pipeline thread per listed device (on a
+    one-GPU box the same device listed 2 and 3 times), the later shards moved
+    behind the earlier ones: bytes and offsets identical to the oracle's for
+    plain 256v32, a chained D1 list (each shard continues from the value
+    before its first block), per-unit starts, 256v64, and fewer blocks than
+    devices."""
+    L = capi()
+    L.tpf_host_enc_multi.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                                     ctypes.c_uint, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                     ctypes.c_uint64, ctypes.c_void_p]
+    ndev = torch.cuda.device_count()
+    blocks = np.concatenate([datagen.c2_blocks(333, bw, 10, seed=4) for bw in (3, 14, 25)])
+    vals, starts = datagen.c3_postings(1001)
+    v64 = datagen.c4_blocks64(301, 37, 5, seed=2)
+    cases = [("256v32 plain", 2, blocks, 0, None, 0, oracle_lib.enc256v32_batch(blocks)),
+             ("256v32 D1 chained", 2, vals, 1, None, int(starts[0]), oracle_lib.enc256v32_batch(vals, starts=starts)),
+             ("256v32 D1 starts", 2, vals, 1, starts, 0, oracle_lib.enc256v32_batch(vals, starts=starts)),
+             ("256v64 plain", 5, v64, 0, None, 0, oracle_lib.enc256v64_batch(v64)),
+             ("2 blocks", 2, blocks[:2], 0, None, 0, oracle_lib.enc256v32_batch(blocks[:2]))]
+    for k in (2, 3):
+        devs = np.array([i % ndev for i in range(k)], dtype=np.int32)
+        for name, fmt, v, d1, st, s0, (exp_p, exp_o) in cases:
+            nb = len(v)
+            out = np.zeros(nb * 2200 + 64, dtype=np.uint8)
+            off = np.zeros(nb + 1, dtype=np.uint64)
+            rc = L.tpf_host_enc_multi(devs.ctypes.data, k, fmt, v.ctypes.data, nb, 256, d1,
+                                      None if st is None else st.ctypes.data, s0, out.ctypes.data, len(out), off.ctypes.data)
+            assert rc == 0, (name, k, L.tpf_last_error())
+            np.testing.assert_array_equal(off, exp_o, err_msg=f"{name} k={k}")
+            assert out[: int(off[-1])].tobytes() == exp_p.tobytes(), (name, k)
+    small = np.zeros(16, dtype=np.uint8)
+    off = np.zeros(len(blocks) + 1, dtype=np.uint64)
+    devs = np.zeros(2, dtype=np.int32)
+    assert L.tpf_host_enc_multi(devs.ctypes.data, 2, 2, blocks.ctypes.data, len(blocks), 256, 0, None, 0, small.ctypes.data,
+                                len(small), off.ctypes.data) == -1

@@ -696,6 +696,107 @@ int tpf_host_enc(int fmt, const void * h_vals, uint64_t nblocks, unsigned n, int
     }
 }
 
+int tpf_host_enc_multi(const int * devs, int ndev, int fmt, const void * h_vals, uint64_t nblocks, unsigned n, int d1,
+                       const void * h_starts, uint64_t start0, uint8_t * h_out, uint64_t out_cap, uint64_t * h_off)
+{
+    try
+    {
+        if (!h_off)
+            throw Err(TPF_EINVAL, "tpf_host_enc_multi: h_off is required");
+        h_off[0] = 0;
+        if (nblocks == 0)
+            return TPF_OK;
+        need_device();
+        int cnt = 0;
+        hc(hipGetDeviceCount(&cnt), "hipGetDeviceCount");
+        if (!devs || ndev < 1 || ndev > 64)
+            throw Err(TPF_EINVAL, "tpf_host_enc_multi: need 1..64 devices");
+        for (int d = 0; d < ndev; ++d)
+            if (devs[d] < 0 || devs[d] >= cnt)
+                throw Err(TPF_EINVAL, "tpf_host_enc_multi: device " + std::to_string(devs[d]) + " is not visible");
+        const size_t es = wide_fmt(fmt) ? 8 : 4;
+        const size_t uv = unit_values(fmt, n);
+        const auto * vals = static_cast<const uint8_t *>(h_vals);
+        std::vector<uint64_t> cut(static_cast<size_t>(ndev) + 1);
+        for (int d = 0; d <= ndev; ++d)
+            cut[d] = nblocks * static_cast<uint64_t>(d) / static_cast<uint64_t>(ndev);
+        // shard d > 0: into its own host buffer (worst case of its blocks), offsets into h_off's slots
+        std::vector<std::vector<uint8_t>> tmp(static_cast<size_t>(ndev));
+        std::vector<std::vector<uint64_t>> toff(static_cast<size_t>(ndev));
+        std::vector<int> rc(static_cast<size_t>(ndev), TPF_OK);
+        std::vector<std::string> msg(static_cast<size_t>(ndev));
+        std::vector<std::thread> th;
+        for (int d = 0; d < ndev; ++d)
+            th.emplace_back([&, d] {
+                const uint64_t b0 = cut[d], nb = cut[d + 1] - cut[d];
+                if (nb == 0)
+                    return;
+                if (hipSetDevice(devs[d]) != hipSuccess)
+                {
+                    rc[d] = TPF_EHIP;
+                    msg[d] = "hipSetDevice failed";
+                    return;
+                }
+                // a chained D1 list (no per-unit starts): shard d starts after the
+                // previous unit's value n-1 (slots past n are padding)
+                uint64_t s0 = start0;
+                if (d1 && !h_starts && b0 > 0)
+                {
+                    s0 = 0;
+                    std::memcpy(&s0, vals + ((b0 - 1) * uv + n - 1) * es, es);
+                }
+                const void * st = (d1 && h_starts) ? static_cast<const uint8_t *>(h_starts) + b0 * es : nullptr;
+                if (d == 0)
+                    rc[d] = tpf_host_enc(fmt, vals, nb, n, d1, st, s0, h_out, out_cap, h_off);
+                else
+                {
+                    try
+                    {
+                        tmp[d].resize(tpf_enc_bound(fmt, nb, n));
+                        toff[d].resize(nb + 1);
+                    }
+                    catch (const std::exception & e)
+                    {
+                        rc[d] = TPF_EHIP;
+                        msg[d] = e.what();
+                        return;
+                    }
+                    rc[d] = tpf_host_enc(fmt, vals + b0 * uv * es, nb, n, d1, st, s0, tmp[d].data(), tmp[d].size(), toff[d].data());
+                }
+                if (rc[d] != TPF_OK)
+                    msg[d] = tpf_last_error(); // thread-local: carried to the caller's thread below
+            });
+        for (std::thread & t : th)
+            t.join();
+        for (int d = 0; d < ndev; ++d)
+            if (rc[d] != TPF_OK)
+                throw Err(rc[d], "tpf_host_enc_multi: shard " + std::to_string(d) + " (device " + std::to_string(devs[d]) + ", blocks " +
+                                     std::to_string(cut[d]) + ".." + std::to_string(cut[d + 1]) + "): " + msg[d]);
+        // move the later shards into place behind the earlier ones
+        for (int d = 1; d < ndev; ++d)
+        {
+            const uint64_t b0 = cut[d], nb = cut[d + 1] - cut[d];
+            if (nb == 0)
+                continue;
+            const uint64_t pos = h_off[b0], total = toff[d][nb];
+            if (pos + total > out_cap)
+                throw Err(TPF_EINVAL, "tpf_host_enc_multi: out_cap too small");
+            par_copy(h_out + pos, tmp[d].data(), total);
+            for (uint64_t i = 1; i <= nb; ++i)
+                h_off[b0 + i] = pos + toff[d][i];
+        }
+        return TPF_OK;
+    }
+    catch (const Err & e)
+    {
+        return report(e, e.code);
+    }
+    catch (const std::exception & e)
+    {
+        return report(e, TPF_EHIP);
+    }
+}
+
 void tpf_host_release(void)
 {
     const FreePause fp; // the frees below wait on every stream of the device

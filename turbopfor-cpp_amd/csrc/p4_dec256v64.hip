@@ -50,8 +50,15 @@ __device__ __forceinline__ void unpack128v64_lane(const uint32_t * lds, uint32_t
     }
 }
 
+// vbyte scratch of a 128-value block: positions and exception counts < 128
+// (round 4: 2 KB per wave instead of 4, one more workgroup per CU)
+#ifndef TPF_D64_POS
+#define TPF_D64_POS 128
+#endif
+constexpr uint32_t kPos64 = TPF_D64_POS;
+
 // Decode one 128v64 block at LDS byte s into lane t's values 2t, 2t+1.
-// Returns the consumed bytes (wave-uniform).  scr: 512 u64 per wave.
+// Returns the consumed bytes (wave-uniform).  scr: 2 * kPos64 u64 per wave.
 __device__ __forceinline__ uint32_t decode_block128v64(const uint32_t * lds, uint32_t s, uint64_t * scr, uint32_t t, uint64_t & x0,
                                                        uint64_t & x1)
 {
@@ -103,7 +110,7 @@ __device__ __forceinline__ uint32_t decode_block128v64(const uint32_t * lds, uin
     if (b == 63u)
         b = 64u;
     unpack128v64_lane(lds, s + 2u, b, t, x0, x1);
-    const uint32_t end = vbyte_exceptions_g<true>(lds, s + 2u + 16u * b, x1b, scr, scr + 256, t);
+    const uint32_t end = vbyte_exceptions_g<true, kPos64>(lds, s + 2u + 16u * b, x1b, scr, scr + kPos64, t);
     x0 |= shl64(scr[2u * t], b);
     x1 |= shl64(scr[2u * t + 1u], b);
     return end - s;
@@ -160,9 +167,21 @@ constexpr uint32_t kRun64 = 16; // units per wave run (both phases: a Prefix run
 #define TPF_D64_SC1NT 0
 #endif
 template <uint32_t NB, Start64 SM>
-__global__ __launch_bounds__(256, 4) void k_dec128v64w(const Dec64Args A)
+// pipeline (A/B knobs): units in flight, one 16-byte load per lane per unit
+// (the 256v32 hot path's ONE layout: the rest of a unit larger than 1 KB is
+// loaded at staging) or two, and the waves per SIMD the launch bounds ask for
+#ifndef TPF_D64_NC
+#define TPF_D64_NC 3
+#endif
+#ifndef TPF_D64_ONE
+#define TPF_D64_ONE 0
+#endif
+#ifndef TPF_D64_MINW
+#define TPF_D64_MINW 4
+#endif
+__global__ __launch_bounds__(256, TPF_D64_MINW) void k_dec128v64w(const Dec64Args A)
 {
-    constexpr uint32_t kRun = kRun64, NC = 3;
+    constexpr uint32_t kRun = kRun64, NC = TPF_D64_NC;
     constexpr bool D1 = SM == Start64::PerUnit || SM == Start64::Prefix;
     const uint8_t * in = A.in;
     const uint64_t in_bytes = A.in_bytes, nunits = A.nunits;
@@ -170,7 +189,7 @@ __global__ __launch_bounds__(256, 4) void k_dec128v64w(const Dec64Args A)
     uint64_t * out = A.out;
     unsigned long long * err = A.err;
     __shared__ uint32_t slots[4][kSlot64 / 4];
-    __shared__ uint64_t scratch[4][512];
+    __shared__ uint64_t scratch[4][2 * kPos64];
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
     uint32_t * slot = slots[wv];
@@ -185,7 +204,7 @@ __global__ __launch_bounds__(256, 4) void k_dec128v64w(const Dec64Args A)
     const uint64_t unit = first + t;
     const uint64_t o = valid ? off[unit] : 0ull;
     const uint64_t e = valid ? off[unit + 1u] : 0ull;
-    RunPlaneT<kSlot64> P;
+    RunPlaneT<kSlot64, TPF_D64_ONE != 0> P;
     P.init(in_base, in_base + in_bytes, o, e, valid);
     uint64_t startv = 0ull;
     if constexpr (SM == Start64::PerUnit)

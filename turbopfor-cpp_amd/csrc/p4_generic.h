@@ -142,14 +142,19 @@ __device__ __forceinline__ uint32_t vbyte_len(uint32_t m)
 
 // vbyte exceptions into scr[pos] (T per position, zeroed here).  Same
 // 64-byte window parse as vbyte_exceptions in p4_block32.h, generic width.
-template <bool Wide>
+// NPOS: scratch entries of scr and of tmp (256; 128 for the 128-value 64-bit
+// blocks, whose valid positions and exception counts are < 128: malformed
+// ones alias inside the scratch instead of leaving it)
+template <bool Wide, uint32_t NPOS = 256>
 __device__ __forceinline__ uint32_t vbyte_exceptions_g(const uint32_t * lds, uint32_t v0, uint32_t xn,
                                                        typename std::conditional<Wide, uint64_t, uint32_t>::type * scr,
                                                        typename std::conditional<Wide, uint64_t, uint32_t>::type * tmp,
                                                        uint32_t t)
 {
     using T = typename std::conditional<Wide, uint64_t, uint32_t>::type;
-    for (uint32_t i = t; i < 256u; i += 64u)
+    static_assert(NPOS == 128u || NPOS == 256u, "scratch of 128 or 256 positions");
+    constexpr uint32_t PM = NPOS - 1u;
+    for (uint32_t i = t; i < NPOS; i += 64u)
         scr[i] = 0;
     wave_lds_sync();
     const uint32_t first = uni(lds_byte(lds, v0));
@@ -161,7 +166,7 @@ __device__ __forceinline__ uint32_t vbyte_exceptions_g(const uint32_t * lds, uin
         for (uint32_t k = t; k < xn; k += 64u)
         {
             const T val = Wide ? static_cast<T>(lds_u64(lds, v0 + 1u + ES * k)) : static_cast<T>(lds_u32(lds, v0 + 1u + ES * k));
-            atomicOr(&scr[lds_byte(lds, pbase + k)], val);
+            atomicOr(&scr[lds_byte(lds, pbase + k) & PM], val);
         }
         vend = pbase;
     }
@@ -179,7 +184,7 @@ __device__ __forceinline__ uint32_t vbyte_exceptions_g(const uint32_t * lds, uin
             const uint32_t pn = bperm(nxt, p); // every lane: bpermute reads 0 from inactive lanes
             const uint32_t pe = p < 64u ? pn : p;
             if (t < cnt)
-                tmp[(found + t) & 255u] = static_cast<T>(vbyte_value<Wide>(lds, c + p, lds_byte(lds, c + p)));
+                tmp[(found + t) & PM] = static_cast<T>(vbyte_value<Wide>(lds, c + p, lds_byte(lds, c + p)));
             const uint32_t e_last = uni(__builtin_amdgcn_readlane(pe, cnt - 1u));
             found += cnt;
             vend = c + e_last;
@@ -188,7 +193,7 @@ __device__ __forceinline__ uint32_t vbyte_exceptions_g(const uint32_t * lds, uin
         }
         wave_lds_sync();
         for (uint32_t k = t; k < xn; k += 64u)
-            atomicOr(&scr[lds_byte(lds, vend + k)], tmp[k]);
+            atomicOr(&scr[lds_byte(lds, vend + k) & PM], tmp[k & PM]);
     }
     wave_lds_sync();
     return vend + xn;
