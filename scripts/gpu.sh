@@ -8,6 +8,7 @@
 #   pmc:WL           FETCH_SIZE and WRITE_SIZE passes (separate runs) + pmc_traffic.py
 #                    -> gpurun_out/pmc_traffic.json (starts from profiles/pmc_traffic.json)
 #   ab:WL            LIBS="tree ablib/x.so" ROUNDS=2: bench per library build
+#   libs:SCRIPT[:ARGS] python SCRIPT once per library build in LIBS     -> ${TAG}_SCRIPT.log
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS (comma list)           -> ${TAG}_SCRIPT.log
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R; mkdir -p gpurun_out
@@ -58,6 +59,17 @@ for f in glob.glob(sys.argv[1] + '/**/*kernel_stats.csv', recursive=True):
           python -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['config']; r=d['roofline']; print(sys.argv[2], d['value'], 'ms', r.get('kernel_ms_avg'), 'verified', c.get('verified'), {k: v for k, v in c.items() if k.endswith('per_s')})" $O/${T}_ab_${n}_$i.json $n
         done
       done ;;
+    libs)
+      # python SCRIPT ARGS once per library build in LIBS (TPF_LIB), ROUNDS times
+      s=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
+      for i in $(seq ${ROUNDS:-2}); do
+        for lib in ${LIBS:-tree}; do
+          if [ $lib = tree ]; then unset TPF_LIB; else export TPF_LIB=$R/$lib; fi
+          timeout -k 10 ${PY_TIMEOUT:-300} python -u $s ${a//,/ } >> $O/${T}_$(basename $s .py).log 2>&1 || fail "libs $s $lib" $? $O/${T}_$(basename $s .py).log
+          tail -1 $O/${T}_$(basename $s .py).log
+        done
+      done
+      unset TPF_LIB ;;
     py)
       s=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
       timeout -k 10 ${PY_TIMEOUT:-300} python -u $s ${a//,/ } > $O/${T}_$(basename $s .py).log 2>&1 || fail "py $s" $? $O/${T}_$(basename $s .py).log

@@ -114,12 +114,16 @@ def lib():
         L.tpf_p4ndec256v32_workspace_size.restype = ctypes.c_size_t
         L.tpf_p4ndec256v32.argtypes = [c_vp, c_u64, c_vp, c_u64, ctypes.c_int, ctypes.c_uint32, c_vp, c_vp,
                                        ctypes.c_size_t, c_vp, c_vp]
-        L.tpf_d1dec64_chain_workspace_size.argtypes = [c_u64]
-        L.tpf_d1dec64_chain_workspace_size.restype = ctypes.c_size_t
-        L.tpf_d1dec64_chained.argtypes = [ctypes.c_int, c_vp, c_u64, c_vp, c_u64, c_vp, c_u64, c_vp, ctypes.c_size_t, c_vp, c_vp]
-        L.tpf_d1dec64_chain_sums.argtypes = [ctypes.c_int, c_vp, c_u64, c_vp, c_u64, c_vp, ctypes.c_size_t, c_vp, c_vp, c_vp]
-        L.tpf_d1dec64_chain_decode.argtypes = [ctypes.c_int, c_vp, c_u64, c_vp, c_u64, c_vp, c_u64, c_vp, c_vp, c_vp]
-        for name in ("tpf_d1dec64_chained", "tpf_d1dec64_chain_sums", "tpf_d1dec64_chain_decode", "tpf_p4nenc256v32", "tpf_p4ndec256v32", "tpf_p4dec256v32_batch", "tpf_p4d1dec256v32_batch", "tpf_p4enc256v32_batch",
+        # round-4 entry points: absent from older builds loaded through TPF_LIB for A/B runs
+        if hasattr(L, "tpf_d1dec64_chained"):
+            L.tpf_d1dec64_chain_workspace_size.argtypes = [c_u64]
+            L.tpf_d1dec64_chain_workspace_size.restype = ctypes.c_size_t
+            L.tpf_d1dec64_chained.argtypes = [ctypes.c_int, c_vp, c_u64, c_vp, c_u64, c_vp, c_u64, c_vp, ctypes.c_size_t, c_vp, c_vp]
+            L.tpf_d1dec64_chain_sums.argtypes = [ctypes.c_int, c_vp, c_u64, c_vp, c_u64, c_vp, ctypes.c_size_t, c_vp, c_vp, c_vp]
+            L.tpf_d1dec64_chain_decode.argtypes = [ctypes.c_int, c_vp, c_u64, c_vp, c_u64, c_vp, c_u64, c_vp, c_vp, c_vp]
+            for name in ("tpf_d1dec64_chained", "tpf_d1dec64_chain_sums", "tpf_d1dec64_chain_decode"):
+                getattr(L, name).restype = ctypes.c_int
+        for name in ("tpf_p4nenc256v32", "tpf_p4ndec256v32", "tpf_p4dec256v32_batch", "tpf_p4d1dec256v32_batch", "tpf_p4enc256v32_batch",
                      "tpf_p4d1enc256v32_batch", "tpf_dec_batch", "tpf_enc_batch", "tpf_p4d1dec256v32_chained",
                      "tpf_p4d1dec256v32_chain_sums", "tpf_p4d1dec256v32_chain_decode", "tpf_probe256v32",
                      "tpf_probe_hbm", "tpf_probe_enc256v32"):
