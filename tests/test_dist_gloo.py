@@ -137,3 +137,54 @@ def test_shard_range_covers():
             rs = [tpf_shard.shard_range(n, w, r) for r in range(w)]
             assert rs[0][0] == 0 and rs[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+
+
+def _global_list64_worker(rank, world, port, nb, q):
+    """bench.py's c3chain64 path on the CPU: rank r's slice of ONE 64-bit
+    posting list (bench_data.gen_c3_64, carry by all-gather), p4D1Enc256v64
+    units (the oracle standing in for the GPU), phase A (unit delta totals
+    mod 2^64), the exchange (tpf_shard.chained_base64), phase B."""
+    import bench_data
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = tpf_shard.shard_range(world * nb, world, rank)
+        start0 = (1 << 40) + 12345
+        vals, starts = bench_data.gen_c3_64(hi - lo, 7, "cpu", first_block=lo,
+                                            carry_fn=lambda tot: tpf_shard.exclusive_prefix(tot, "cpu"), start0=start0)
+        v = vals.numpy().view(np.uint64)
+        st = starts.numpy().view(np.uint64)
+        packed, off = oracle_lib.enc256v64_batch(v, starts=st)
+        raw = oracle_lib.dec256v64_batch(packed, off, hi - lo, starts=np.zeros(hi - lo, np.uint64))
+        sums = raw[:, -1].astype(np.uint64)  # each unit's total from start 0
+        with np.errstate(over="ignore"):
+            total = int(sums.sum(dtype=np.uint64))
+        base = tpf_shard.chained_base64(torch.tensor([total - (1 << 64) if total >= 1 << 63 else total]), start0=start0)
+        with np.errstate(over="ignore"):
+            pref = np.concatenate([[0], np.cumsum(sums, dtype=np.uint64)[:-1]]).astype(np.uint64) + np.uint64(base)
+        got = oracle_lib.dec256v64_batch(packed, off, hi - lo, starts=pref)
+        ok = bool(np.array_equal(got, v)) and base == int(st[0])
+        q.put((rank, ok, tpf_shard.all_ok(ok, "cpu"), base))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_global_posting_list64_across_ranks(world):
+    """The 64-bit chained list across ranks: one u64 total per rank
+    all-gathered (mod 2^64), every rank's slice rebuilt exactly."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_global_list64_worker, args=(r, world, port, 24, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(r[1] for r in res), res
+    assert all(r[2] for r in res)
+    assert res[0][3] == (1 << 40) + 12345 and all(r[3] > res[0][3] for r in res[1:])
