@@ -9,7 +9,7 @@
 //
 // Grid-stride over 16-byte vectors, 256-thread workgroups, 128 workgroups per
 // CU (the best of 32/128 per CU in scripts/hbm_probe.hip,
-// profiles/r1_v3_hbm_probes.txt).
+// profiles/archive/r1/r1_v3_hbm_probes.txt).
 #include <hip/hip_runtime.h>
 
 #include "tpf_device.h"
