@@ -96,6 +96,24 @@ def test_pageable_host_streams_then_torch_copies(monkeypatch):
         except Exception as e:  # noqa: BLE001
             errors.append(repr(e))
 
+    # small pageable device-to-host reads (torch's .item()) of known values:
+    # with stale page-locked ranges a DMA lands in physical pages the address
+    # no longer maps (the round-3 library's symptom: err read back as a byte
+    # pattern that was never written)
+    sentinel = torch.tensor([0x0123456789ABCDEF, -2], dtype=torch.int64, device=DEV)
+    pinned = torch.empty(1, dtype=torch.int64).pin_memory()
+
+    def check_replay(it):
+        gout.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(gout, gvals), it
+        pinned.copy_(gerr)  # pinned: DMA straight into a page-locked buffer
+        assert int(pinned.item()) == -1, (it, "pinned read", hex(int(pinned.item()) & ((1 << 64) - 1)))
+        assert int(sentinel[0].item()) == 0x0123456789ABCDEF and int(sentinel[1].item()) == -2, (it, "sentinel")
+        assert int(gerr.item()) == -1, (it, "pageable read", hex(int(gerr.item()) & ((1 << 64) - 1)))
+
+    check_replay(-1)  # before any host-stream call
     th = threading.Thread(target=per_block)
     th.start()
     try:
@@ -133,11 +151,7 @@ def test_pageable_host_streams_then_torch_copies(monkeypatch):
             bw = torch.randint(1, 33, (gvals.shape[0], 1), device=DEV, generator=gen)
             raw = torch.randint(-(1 << 31), (1 << 31) - 1, gvals.shape, device=DEV, generator=gen, dtype=torch.int32)
             gvals.copy_(torch.where(bw >= 32, raw, raw & ((torch.ones_like(bw) << bw) - 1).to(torch.int32)))
-            gout.zero_()
-            g.replay()
-            torch.cuda.synchronize()
-            assert torch.equal(gout, gvals), it
-            assert int(gerr.item()) == -1
+            check_replay(it)
     finally:
         stop.set()
         th.join(timeout=60)

@@ -62,7 +62,13 @@ struct DecArgs
 // Measured and kept: runs of 16 (8: same, 32..62:
 // -2..-5%), 7 waves/SIMD; ONE/NC=6 beat two loads/NC=3 by 1-2% (C2) and
 // 2-6% (C3); deeper pipelines lose occupancy.
-template <StartMode SM, uint32_t kRun, uint32_t POL = 2, uint32_t NC = 3, int MINW = 7, bool ONE = false>
+// GB != 0 (round 4, A/B knob TPF_DEC_GROUP): the pipeline moves GROUPS of
+// consecutive blocks whose bytes fit one GB-byte window from the first
+// block's 16-aligned start (one ballot per group: block ends ascend) instead
+// of single blocks, so a wave keeps ~NC KB of reads in flight whatever the
+// block size (a 166-byte bw-1 block uses 11 of 64 lanes of its own load);
+// a group of one block larger than the window takes the big-block path.
+template <StartMode SM, uint32_t kRun, uint32_t POL = 2, uint32_t NC = 3, int MINW = 7, bool ONE = false, uint32_t GB = 0>
 __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
 {
     __shared__ uint32_t slots[4][kSlotBytes / 4];
@@ -89,7 +95,36 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
     const uint64_t o = valid ? A.off[blk] : 0ull;
     const uint64_t e = valid ? A.off[blk + 1u] : 0ull;
     RunPlaneT<kSlotBytes, ONE> P;
-    P.init(in_base, in_end, o, e, valid);
+    // groups (GB != 0): lane g = group g (first block, block count); the plane holds groups
+    uint32_t gfb = 0u, gcnt = 0u, ng = n, blen = 0u, ablo = 0u;
+    if constexpr (GB != 0u)
+    {
+        static_assert(ONE && stride == 1u && kRun <= 64u && GB <= 1024u, "groups: one load per lane, contiguous runs");
+        blen = (e >= o && e - o < 0x10000ull) ? static_cast<uint32_t>(e - o) : 0xFFFFFFFFu;
+        const uint64_t ab = in_base + o;
+        ablo = static_cast<uint32_t>(ab);
+        ng = 0u;
+        for (uint32_t j = 0; j < n;)
+        {
+            const uint64_t cb = readlane_u64(ab, j) & ~15ull;
+            const uint64_t fit = __ballot(valid && t >= j && e >= o && in_base + e <= cb + GB) >> j;
+            uint32_t c = static_cast<uint32_t>(__builtin_ctzll(~fit)); // consecutive fitting blocks from j
+            c = c == 0u ? 1u : c;                                      // a big (or implausible) block alone
+            gfb = t == ng ? j : gfb;
+            gcnt = t == ng ? c : gcnt;
+            ++ng;
+            j += c;
+        }
+        const bool gvalid = t < ng;
+        const uint32_t l0 = gfb & 63u, l1 = (gfb + gcnt - 1u) & 63u;
+        const uint64_t go = (static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(o >> 32)), static_cast<int>(l0), 64))) << 32)
+                            | static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(o)), static_cast<int>(l0), 64));
+        const uint64_t ge = (static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(e >> 32)), static_cast<int>(l1), 64))) << 32)
+                            | static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(e)), static_cast<int>(l1), 64));
+        P.init(in_base, in_end, gvalid ? go : 0ull, gvalid ? ge : 0ull, gvalid);
+    }
+    else
+        P.init(in_base, in_end, o, e, valid);
     uint32_t startv = 0u;
     if constexpr (SM == StartMode::PerBlock)
         startv = valid ? A.starts[blk] : 0u;
@@ -124,6 +159,34 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
 
     auto issue = [&](Chunk & c, uint32_t jj) { P.template issue<POL>(c, jj, t); };
     auto consume = [&](const Chunk & c, uint32_t jj) {
+        if constexpr (GB != 0u)
+        {
+            // group jj: its blocks decoded one after another from the staged window
+            const uint32_t fb = rl(gfb, jj), cnt = rl(gcnt, jj);
+            if constexpr (SM == StartMode::Probe)
+            {
+                const u32x4 x = c.a | P.big_rest_or(jj, t);
+                for (uint32_t k = 0; k < cnt; ++k)
+                    put(fb + k, x);
+                return;
+            }
+            P.stage(c, jj, slot, t);
+            const uint32_t cblo = rl(P.cblo, jj);
+            for (uint32_t k = 0; k < cnt; ++k)
+            {
+                const uint32_t b = fb + k;
+                const uint32_t sb = rl(ablo, b) - cblo; // the block's start inside the window
+                u32x4 v;
+                const uint32_t used = decode_block256v32(slot, sb, uni(lds_u32(slot, sb)), scr, t, v);
+                if constexpr (SM == StartMode::PerBlock || SM == StartMode::Prefix)
+                    apply_delta1_256(v, rl(startv, b));
+                put(b, v);
+                wave_lds_sync();
+                if (used != rl(blen, b))
+                    badmask |= 1ull << b;
+            }
+            return;
+        }
         if constexpr (SM == StartMode::Probe)
         {
             put(jj, ONE ? (c.a | P.big_rest_or(jj, t)) : (c.a | c.b));
@@ -157,7 +220,7 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
                 {
                     issue(C[(u + NC - 1) % NC], j + u + NC - 1);
                     consume(C[u], j + u);
-                    more = j + u + 1 < n;
+                    more = j + u + 1 < ng;
                 }
             }
         }
@@ -412,12 +475,20 @@ namespace
 #ifndef TPF_DEC_POL
 #define TPF_DEC_POL (2 | 8)
 #endif
+// grouped loads (A/B knob, 0 = one load per block): window bytes and run length
+#ifndef TPF_DEC_GROUP
+#define TPF_DEC_GROUP 0
+#endif
+#ifndef TPF_DEC_GROUP_RUN
+#define TPF_DEC_GROUP_RUN 32
+#endif
 template <dev::StartMode SM>
 hipError_t launch_mode(const dev::DecArgs & A, hipStream_t stream)
 {
-    constexpr uint64_t per_wg = 4ull * dev::kRunDefault;
+    constexpr uint32_t run = TPF_DEC_GROUP ? TPF_DEC_GROUP_RUN : dev::kRunDefault;
+    constexpr uint64_t per_wg = 4ull * run;
     const uint32_t grid = static_cast<uint32_t>((A.nblocks + per_wg - 1) / per_wg);
-    hipLaunchKernelGGL((dev::k_dec256v32w<SM, dev::kRunDefault, TPF_DEC_POL, 6, 7, true>), dim3(grid), dim3(256), 0, stream, A);
+    hipLaunchKernelGGL((dev::k_dec256v32w<SM, run, TPF_DEC_POL, 6, 7, true, TPF_DEC_GROUP>), dim3(grid), dim3(256), 0, stream, A);
     return hipGetLastError();
 }
 } // namespace
