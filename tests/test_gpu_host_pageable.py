@@ -68,7 +68,10 @@ def _graph(L, nb):
     return g, vals, out, err, (packed, offs, ws)
 
 
-def test_pageable_host_streams_then_torch_copies(monkeypatch):
+@pytest.mark.parametrize("host_calls", [False, True], ids=["graph-only", "host-streams"])
+def test_pageable_host_streams_then_torch_copies(monkeypatch, host_calls):
+    """host_calls=False: the same replays and torch copies without any
+    host-stream call (tells a kernel-side overrun from host-stream effects)."""
     monkeypatch.setenv("TPF_HOST_CHUNK_BYTES", str(192 * 1024))  # many pipeline chunks per call
     L = _abi()
     rng = np.random.default_rng(41)
@@ -123,6 +126,19 @@ def test_pageable_host_streams_then_torch_copies(monkeypatch):
             packed = exp_packed[: exp_off[nb]].copy()
             off = exp_off[: nb + 1].copy()
             back = np.empty_like(blocks)
+            if not host_calls:
+                sizes = (back.nbytes, nb * 1100 + 64, packed.nbytes, blocks.nbytes)
+                del blocks, packed, off, back
+                for sz in sizes:
+                    x = rng.integers(0, 256, sz, dtype=np.uint8)
+                    d = torch.from_numpy(x).to(DEV)
+                    assert np.array_equal(d.cpu().numpy(), x)
+                    del d
+                bw = torch.randint(1, 33, (gvals.shape[0], 1), device=DEV, generator=gen)
+                raw = torch.randint(-(1 << 31), (1 << 31) - 1, gvals.shape, device=DEV, generator=gen, dtype=torch.int32)
+                gvals.copy_(torch.where(bw >= 32, raw, raw & ((torch.ones_like(bw) << bw) - 1).to(torch.int32)))
+                check_replay(it)
+                continue
             assert L.tpf_host_dec(2, packed.ctypes.data, len(packed), off.ctypes.data, nb, 256, back.ctypes.data,
                                   None) == 0, L.tpf_last_error()
             np.testing.assert_array_equal(back, blocks)
