@@ -15,6 +15,7 @@ graph, each result checked exactly.
 """
 import ctypes
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -96,6 +97,7 @@ def test_pageable_host_streams_then_torch_copies(monkeypatch, host_calls):
                     assert L.tpf_p4Dec256v32(buf.ctypes.data, 256, out.ctypes.data) == end
                     assert np.array_equal(out, v)
                     calls[0] += 1
+                    time.sleep(0.0005)  # leave the GIL to the main thread (the server idles out after 10 ms)
         except Exception as e:  # noqa: BLE001
             errors.append(repr(e))
 
