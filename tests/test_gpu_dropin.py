@@ -522,3 +522,52 @@ def test_host_enc_multi_vs_single():
     devs = np.zeros(2, dtype=np.int32)
     assert L.tpf_host_enc_multi(devs.ctypes.data, 2, 2, blocks.ctypes.data, len(blocks), 256, 0, None, 0, small.ctypes.data,
                                 len(small), off.ctypes.data) == -1
+
+
+def test_device_synchronize_beside_busy_per_block_caller():
+    """A thread issuing per-block calls back to back keeps the resident block
+    server busy; hipDeviceSynchronize (torch.cuda.synchronize) in another
+    thread waits for every stream of the device, the server's included.  The
+    server leaves after 5 ms of service even when busy (the next call
+    relaunches it), so such waits return promptly instead of never (round 4:
+    found with scripts/graph_canary.py)."""
+    import threading
+    import time
+
+    L = capi()
+    L.tpf_p4Enc256v32.restype = ctypes.c_void_p
+    L.tpf_p4Enc256v32.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]
+    L.tpf_p4Dec256v32.restype = ctypes.c_void_p
+    L.tpf_p4Dec256v32.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]
+    stop = threading.Event()
+    errors, calls = [], [0]
+    v = np.ascontiguousarray(datagen.c2_blocks(1, 12, 10, seed=6)[0])
+
+    def busy():
+        try:
+            buf = np.zeros(4096, np.uint8)
+            out = np.zeros(256, np.uint32)
+            while not stop.is_set():
+                end = L.tpf_p4Enc256v32(v.ctypes.data, 256, buf.ctypes.data)
+                assert L.tpf_p4Dec256v32(buf.ctypes.data, 256, out.ctypes.data) == end
+                calls[0] += 1
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = threading.Thread(target=busy)
+    th.start()
+    try:
+        time.sleep(0.05)
+        x = torch.arange(1 << 20, device="cuda", dtype=torch.int64)
+        t0 = time.time()
+        for _ in range(20):
+            x.add_(1)
+            torch.cuda.synchronize()
+        dt = time.time() - t0
+    finally:
+        stop.set()
+        th.join(timeout=60)
+    assert not errors, errors
+    assert calls[0] > 0
+    assert dt < 10.0, f"20 device-wide synchronizes took {dt:.1f} s beside a busy per-block caller"
+    assert int(x[0].item()) == 20

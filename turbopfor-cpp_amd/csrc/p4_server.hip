@@ -12,8 +12,10 @@
 // in pinned host memory and acknowledges.  Host and device exchange only
 // plain loads and stores ordered by system-scope fences (no atomics on
 // shared memory).  Exit: every wave leaves once all mailboxes have been idle
-// for idle_ticks of the 100 MHz real-time counter, or at once when the host
-// sets `stop`; `alive` drops and the host relaunches on the next call.
+// for idle_ticks of the 100 MHz real-time counter, after max_ticks in any
+// case (a device-wide synchronize elsewhere in the process must not wait for
+// it forever), or at once when the host sets `stop`; `alive` drops and the
+// host relaunches on the next call.
 #include <hip/hip_runtime.h>
 
 #include "p4_generic.h"
@@ -156,16 +158,17 @@ __device__ __forceinline__ void srv_serve(SrvLds & L, const ServerReqBox * box, 
         ans->result = size;
 }
 
-__global__ __launch_bounds__(256) void k_block_server(ServerReq * rq, ServerAns * an, uint64_t idle_ticks)
+__global__ __launch_bounds__(256) void k_block_server(ServerReq * rq, ServerAns * an, uint64_t idle_ticks, uint64_t max_ticks)
 {
     __shared__ SrvLds L[kServerBoxes];
     __shared__ uint64_t last_active;
     __shared__ uint32_t quit;
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t w = uni(threadIdx.x >> 6);
+    const uint64_t born = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0)
     {
-        last_active = __builtin_amdgcn_s_memrealtime();
+        last_active = born;
         quit = 0u;
     }
     if (threadIdx.x == 0)
@@ -224,12 +227,19 @@ __global__ __launch_bounds__(256) void k_block_server(ServerReq * rq, ServerAns 
             if (t == 0)
                 atomicMax(reinterpret_cast<unsigned long long *>(&last_active),
                           static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+            if (__builtin_amdgcn_s_memrealtime() - born > max_ticks) // busy past the lifetime: leave after this answer
+            {
+                if (t == 0)
+                    quit = 1u;
+                break;
+            }
             continue;
         }
         // leave together: once one wave quits (idle or told to stop) the others follow
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
         // (the stop word is read every 64th poll: each read is a PCIe round trip)
-        if (uni(quit) != 0u || ((polls & 63u) == 0u && uni(ld_sys(&rq->stop)) != 0u) || now - last_active > idle_ticks)
+        if (uni(quit) != 0u || ((polls & 63u) == 0u && uni(ld_sys(&rq->stop)) != 0u) || now - last_active > idle_ticks ||
+            now - born > max_ticks)
         {
             if (t == 0)
                 quit = 1u;
@@ -250,7 +260,7 @@ namespace tpf
 
 hipError_t launch_block_server(ServerReq * d_req, ServerAns * d_ans, hipStream_t s)
 {
-    hipLaunchKernelGGL(dev::k_block_server, dim3(1), dim3(256), 0, s, d_req, d_ans, kServerIdleTicks);
+    hipLaunchKernelGGL(dev::k_block_server, dim3(1), dim3(256), 0, s, d_req, d_ans, kServerIdleTicks, kServerMaxTicks);
     return hipGetLastError();
 }
 

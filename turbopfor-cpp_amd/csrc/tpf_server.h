@@ -31,6 +31,13 @@ namespace tpf
 constexpr uint32_t kServerBoxes = 4;           // one wave per mailbox, one workgroup
 constexpr uint32_t kServerPayload = 8192;      // bytes in / out per request
 constexpr uint64_t kServerIdleTicks = 1000000; // 10 ms of s_memrealtime (100 MHz)
+// A launch also leaves after serving for 5 ms, busy or not (the next call
+// relaunches it, ~20 us per 5 ms of traffic): hipDeviceSynchronize -- e.g.
+// torch.cuda.synchronize() in another thread -- waits for every stream of the
+// device, the server's included, and under back-to-back per-block calls an
+// unbounded launch never idled out, so such a wait never returned (round 4,
+// scripts/graph_canary.py with a per-block caller thread).
+constexpr uint64_t kServerMaxTicks = 500000;
 
 enum : uint32_t
 {
