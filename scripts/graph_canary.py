@@ -1,7 +1,8 @@
 """Diagnostic (measurement tool): the 256v32 encode + decode batch pair on
 random data, eager and captured into a hipGraph, with every buffer carved out
 of ONE arena with 4 KB canary zones between them, with or without the
-per-block block server running in another thread.  After each call the
+per-block block server running in another thread (or another thread launching
+plain torch kernels).  After each call the
 canaries must be intact and d_err must read -1.  Prints one line per mode.
 usage: python scripts/graph_canary.py [nblocks] [iters]"""
 import ctypes
@@ -86,6 +87,17 @@ def per_block():
         time.sleep(0.001)
 
 
+def launcher():
+    """another thread launching ordinary torch kernels on a stream of its own"""
+    st = torch.cuda.Stream()
+    y = torch.zeros(1 << 16, dtype=torch.int64, device=DEV)
+    with torch.cuda.stream(st):
+        while not srv_stop.is_set():
+            y.add_(1)
+            time.sleep(0.001)
+    st.synchronize()
+
+
 def run(mode, server):
     nbad, nerr, nval, first = 0, 0, 0, None
     g = None
@@ -99,7 +111,7 @@ def run(mode, server):
     th = None
     if server:
         srv_stop.clear()
-        th = threading.Thread(target=per_block)
+        th = threading.Thread(target=per_block if server == "perblock" else launcher)
         th.start()
     for it in range(iters):
         vals.copy_(fresh())
@@ -123,7 +135,6 @@ def run(mode, server):
 
 
 print(f"nblocks={nb} layout={layout}", flush=True)
-for mode in ("eager", "graph"):
-    for server in (False, True):
-        run(mode, server)
+for mode, server in (("eager", None), ("eager", "perblock"), ("graph", None), ("graph", "perblock"), ("graph", "launcher")):
+    run(mode, server)
 print("done", flush=True)

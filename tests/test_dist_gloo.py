@@ -163,7 +163,7 @@ def _global_list64_worker(rank, world, port, nb, q):
             total = int(sums.sum(dtype=np.uint64))
         base = tpf_shard.chained_base64(torch.tensor([total - (1 << 64) if total >= 1 << 63 else total]), start0=start0)
         with np.errstate(over="ignore"):
-            pref = np.concatenate([[0], np.cumsum(sums, dtype=np.uint64)[:-1]]).astype(np.uint64) + np.uint64(base)
+            pref = np.concatenate([np.zeros(1, np.uint64), np.cumsum(sums, dtype=np.uint64)[:-1]]) + np.uint64(base)
         got = oracle_lib.dec256v64_batch(packed, off, hi - lo, starts=pref)
         ok = bool(np.array_equal(got, v)) and base == int(st[0])
         q.put((rank, ok, tpf_shard.all_ok(ok, "cpu"), base))

@@ -58,11 +58,11 @@ def test_chained64_vs_oracle_sequential(fmt, nu):
     width = 256 if fmt == "256v64" else 128
     start0 = (1 << 32) - 1000  # the first unit already crosses 2^32
     vals = _list(nu, width, seed=nu, start0=start0)
-    starts = np.concatenate([[start0], vals[:-1, -1]]).astype(np.uint64)
+    starts = np.concatenate([np.array([start0], dtype=np.uint64), vals[:-1, -1]])  # (a Python int + uint64 would go float64)
     exp_bytes = b"".join(oracle_lib.encode(fmt, vals[i], d1=True, start=int(starts[i])) for i in range(nu))
     packed, offs = tpf.enc_batch(fmt, _dev64(vals.ravel()), nu, width, d1=True, start0=start0)
     pk = packed.cpu().numpy()
-    assert pk.tobytes() == exp_bytes
+    assert np.array_equal(pk, np.frombuffer(exp_bytes, dtype=np.uint8)), "GPU bytes differ from the oracle's"
     exp = _oracle_sequential(fmt, pk, offs.cpu().numpy(), nu, width, start0)
     np.testing.assert_array_equal(exp, vals)
     err = torch.zeros(1, dtype=torch.int64, device=DEV)

@@ -516,7 +516,7 @@ def test_host_enc_multi_vs_single():
                                       None if st is None else st.ctypes.data, s0, out.ctypes.data, len(out), off.ctypes.data)
             assert rc == 0, (name, k, L.tpf_last_error())
             np.testing.assert_array_equal(off, exp_o, err_msg=f"{name} k={k}")
-            assert out[: int(off[-1])].tobytes() == exp_p.tobytes(), (name, k)
+            assert np.array_equal(out[: int(off[-1])], exp_p), (name, k)
     small = np.zeros(16, dtype=np.uint8)
     off = np.zeros(len(blocks) + 1, dtype=np.uint64)
     devs = np.zeros(2, dtype=np.int32)

@@ -42,8 +42,8 @@ int prep_err(uint64_t * d_err, hipStream_t s)
 {
     if (!d_err)
         return TPF_OK;
-    hipError_t e = hipMemsetAsync(d_err, 0xFF, sizeof(uint64_t), s);
-    return e == hipSuccess ? TPF_OK : hip_fail(e, "hipMemsetAsync(d_err)");
+    hipError_t e = tpf::fill_u32(d_err, 0xFFFFFFFFu, 2, s);
+    return e == hipSuccess ? TPF_OK : hip_fail(e, "init d_err");
 }
 } // namespace
 
@@ -489,7 +489,7 @@ int tpf_p4ndec256v32(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d
             starts = d_out + nfull * 256 - 1;
         else
         {
-            hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(start), static_cast<int>(start0), 1, s);
+            hipError_t e = tpf::fill_u32(start, start0, 1, s);
             if (e != hipSuccess)
                 return hip_fail(e, "tpf_p4ndec256v32");
             starts = start;

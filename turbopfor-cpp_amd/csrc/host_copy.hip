@@ -69,6 +69,19 @@ __global__ __launch_bounds__(256) void k_append(uint8_t * __restrict__ dst, cons
         *pos_out = p + n;
 }
 
+// p[0 .. n) = v (n <= 64 dwords): the device-side initialisations of the
+// batch entry points (d_err = ~0, empty totals and offsets) as a kernel
+// rather than hipMemsetAsync.  Captured into a hipGraph a memset becomes a
+// memset node, and replays of those nodes wrote a foreign byte pattern
+// (0x11.., 0xd3..) while another thread of the process launched kernels
+// (the block server): scripts/graph_canary.py, DESIGN.md 7.  A kernel node
+// carries its value in its own arguments.
+__global__ void k_fill_u32(uint32_t * p, uint32_t v, uint32_t n)
+{
+    if (threadIdx.x < n)
+        p[threadIdx.x] = v;
+}
+
 // *err = min(*err, base + *sub_err) when the sub-batch reported a block.
 __global__ void k_err_merge(unsigned long long * err, const unsigned long long * sub_err, uint64_t base)
 {
@@ -86,6 +99,16 @@ hipError_t launch_append(uint8_t * dst, const uint8_t * src, const uint64_t * po
                          hipStream_t s)
 {
     hipLaunchKernelGGL(dev::k_append, dim3(1), dim3(256), 0, s, dst, src, pos, len, pos_out);
+    return hipGetLastError();
+}
+
+hipError_t fill_u32(void * p, uint32_t v, uint32_t n, hipStream_t s)
+{
+    if (n == 0)
+        return hipSuccess;
+    if (n > 64u)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(dev::k_fill_u32, dim3(1), dim3(64), 0, s, static_cast<uint32_t *>(p), v, n);
     return hipGetLastError();
 }
 

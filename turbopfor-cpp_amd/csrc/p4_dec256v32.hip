@@ -535,7 +535,7 @@ hipError_t launch_d1chain_sums(const uint8_t * in, uint64_t in_bytes, const uint
                                uint32_t * total, unsigned long long * err, hipStream_t stream)
 {
     if (nblocks == 0)
-        return total ? hipMemsetAsync(total, 0, 4, stream) : hipSuccess;
+        return total ? fill_u32(total, 0u, 1, stream) : hipSuccess;
     if (nblocks > 0x7FFFFFFFull || ws_bytes < d1chain_workspace(nblocks))
         return hipErrorInvalidValue;
     auto * sums = static_cast<uint32_t *>(ws);

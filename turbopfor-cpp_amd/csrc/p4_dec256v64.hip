@@ -360,7 +360,7 @@ hipError_t launch_d1chain64_sums(uint32_t nb, const uint8_t * in, uint64_t in_by
                                  size_t ws_bytes, uint64_t * total, unsigned long long * err, hipStream_t s)
 {
     if (nunits == 0)
-        return total ? hipMemsetAsync(total, 0, 8, s) : hipSuccess;
+        return total ? fill_u32(total, 0u, 2, s) : hipSuccess;
     if (ws_bytes < d1chain64_workspace(nunits))
         return hipErrorInvalidValue;
     const Chain64Ws w = Chain64Ws::carve(ws, nunits);

@@ -23,7 +23,7 @@ hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_
                             int probe)
 {
     if (nblocks == 0)
-        return hipMemsetAsync(off, 0, sizeof(uint64_t), stream);
+        return fill_u32(off, 0u, 2, stream);
     if (nblocks + 1 > 0x7FFFFFFFull || ws_bytes < enc256v32_workspace(nblocks))
         return hipErrorInvalidValue;
     switch (probe)

@@ -459,7 +459,7 @@ hipError_t launch_enc128v64(uint32_t nb, const uint64_t * in, uint64_t nunits, b
                             uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t s)
 {
     if (nunits == 0)
-        return hipMemsetAsync(off, 0, sizeof(uint64_t), s);
+        return fill_u32(off, 0u, 2, s);
     if (nunits + 1 > 0x7FFFFFFFull)
         return hipErrorInvalidValue;
     if (nb == 2u)

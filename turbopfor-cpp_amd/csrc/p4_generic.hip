@@ -682,7 +682,7 @@ hipError_t launch_enc_generic(int fmt, const void * in, uint64_t nblocks, uint32
                               uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t s)
 {
     if (nblocks == 0)
-        return hipMemsetAsync(off, 0, sizeof(uint64_t), s);
+        return fill_u32(off, 0u, 2, s);
     if (nblocks + 1 > 0x7FFFFFFFull)
         return hipErrorInvalidValue;
     switch (fmt)

@@ -1,6 +1,7 @@
 // p4_scan.hip -- the run-total scan of p4_scan.h: two small kernels over one
 // entry per wave run (10M units in runs of 16: 625K entries, 153 tiles).
 #include "p4_scan.h"
+#include "tpf_kernels.h"
 
 namespace tpf::dev
 {
@@ -118,7 +119,7 @@ template <class T, class TT = uint32_t>
 hipError_t run_scan(const TT * tot, uint64_t nruns, T * pre, T * tile, T * total, hipStream_t s, const uint32_t * gate = nullptr)
 {
     if (nruns == 0)
-        return total ? hipMemsetAsync(total, 0, sizeof(T), s) : hipSuccess;
+        return total ? fill_u32(total, 0u, sizeof(T) / 4u, s) : hipSuccess;
     const uint64_t ntiles = RunScanWs<T>::tiles(nruns);
     hipLaunchKernelGGL((dev::k_run_scan_tiles<T, TT>), dim3(static_cast<uint32_t>(ntiles)), dim3(256), 0, s, tot, nruns, pre, tile, gate);
     hipError_t e = hipGetLastError();

@@ -44,6 +44,8 @@ hipError_t launch_copy(void * dst, const void * src, uint64_t bytes, hipStream_t
 hipError_t launch_append(uint8_t * dst, const uint8_t * src, const uint64_t * pos, const uint64_t * len, uint64_t * pos_out,
                          hipStream_t s);
 hipError_t launch_err_merge(unsigned long long * err, const unsigned long long * sub_err, uint64_t base, hipStream_t s);
+// p[0 .. n) = v, n <= 64 dwords, as a kernel (not a memset: see host_copy.hip)
+hipError_t fill_u32(void * p, uint32_t v, uint32_t n, hipStream_t s);
 // Per-block block server (p4_server.hip, tpf_server.h).
 struct ServerReq;
 struct ServerAns;
