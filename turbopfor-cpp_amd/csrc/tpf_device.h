@@ -113,16 +113,18 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
     return x;
 }
 
+// 64-bit inclusive scan (mod 2^64) from three 32-bit DPP scans: x = H 2^32 +
+// M 2^16 + L with 16-bit M and L, whose scans over 64 lanes stay below 2^22
+// (exact), and H scanned mod 2^32; then (SH << 32) + (SM << 16) + SL mod 2^64
+// is the exact scan.  (Round 4: it replaced six 64-bit __shfl_up steps, i.e.
+// twelve ds_bpermute through the LDS pipe, per scan: every 64-bit delta-1
+// block and the 64-bit chained decode's unit sums pay one.)
 __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t x)
 {
-    // 64-bit scan from two 32-bit passes is not associative-safe; use shuffles.
-    for (uint32_t d = 1; d < 64; d <<= 1)
-    {
-        uint64_t y = __shfl_up(x, d, 64);
-        if (lane_id() >= d)
-            x += y;
-    }
-    return x;
+    const uint32_t sh = wave_incl_scan(static_cast<uint32_t>(x >> 32));
+    const uint32_t sm = wave_incl_scan(static_cast<uint32_t>(x >> 16) & 0xFFFFu);
+    const uint32_t sl = wave_incl_scan(static_cast<uint32_t>(x) & 0xFFFFu);
+    return (static_cast<uint64_t>(sh) << 32) + (static_cast<uint64_t>(sm) << 16) + sl;
 }
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x)
