@@ -169,15 +169,18 @@ constexpr uint32_t kRun64 = 16; // units per wave run (both phases: a Prefix run
 template <uint32_t NB, Start64 SM>
 // pipeline (A/B knobs): units in flight, one 16-byte load per lane per unit
 // (the 256v32 hot path's ONE layout: the rest of a unit larger than 1 KB is
-// loaded at staging) or two, and the waves per SIMD the launch bounds ask for
+// loaded at staging) or two, and the waves per SIMD the launch bounds ask for.
+// Round-4 A/B on C4 (profiles/r4f_d64_time.log): ONE + 4 in flight + 6 waves
+// 457 G int64/s, ONE + 6 in flight 456, 4 in flight alone 448, the earlier
+// TWO + 3 + 4 waves 445.
 #ifndef TPF_D64_NC
-#define TPF_D64_NC 3
+#define TPF_D64_NC 4
 #endif
 #ifndef TPF_D64_ONE
-#define TPF_D64_ONE 0
+#define TPF_D64_ONE 1
 #endif
 #ifndef TPF_D64_MINW
-#define TPF_D64_MINW 4
+#define TPF_D64_MINW 6
 #endif
 __global__ __launch_bounds__(256, TPF_D64_MINW) void k_dec128v64w(const Dec64Args A)
 {

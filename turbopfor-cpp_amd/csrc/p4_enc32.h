@@ -366,39 +366,40 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
     wave_lds_sync();
     pack_base_runs<PAD>(img, pw, val, b, t);
     const uint32_t v0 = sb + 2u + 32u * b;
-    // Lane-parallel exception emission (round 4): the lane's i-th flagged
-    // value is taken from its flag mask (lowest set bit, cleared after use),
-    // its byte address is its rank (raw: 4 bytes each) or a wave scan of the
-    // vbyte lengths, and every value is OR-ed into the image as a whole (up to
-    // 8-byte) window of dwords -- no per-value branches, no exec-mask
-    // sections: the write pass is issue-bound and a vbyte-heavy block (C3)
-    // spent its time in per-lane divergent or_bits calls.
+    // Exception emission (round 4): the lane's i-th flagged value is taken
+    // from its flag mask (lowest set bit, cleared after use), its byte address
+    // is its rank (raw: 4 bytes each) or a wave scan of the vbyte lengths, and
+    // only the lanes that hold an i-th exception store its bytes -- plain LDS
+    // byte stores (every byte of the exception area has exactly one writer and
+    // the base payload ends before v0), no atomics and no per-length branches
+    // around the value arithmetic.  A round-4 variant that let every lane OR a
+    // zero into the image (no exec sections) was 27% slower on C3: the idle
+    // lanes' atomics hit the dword of the lane next to them.
     // the most exceptions any lane holds (wave-uniform loop bound)
     const uint32_t mc = __builtin_amdgcn_ballot_w64(cnt >= 4u) ? 4u
                         : __builtin_amdgcn_ballot_w64(cnt >= 3u) ? 3u
                         : __builtin_amdgcn_ballot_w64(cnt >= 2u) ? 2u
                         : __builtin_amdgcn_ballot_w64(cnt >= 1u) ? 1u : 0u;
     auto pick = [&](uint32_t j) { return j == 0u ? ex[0] : j == 1u ? ex[1] : j == 2u ? ex[2] : ex[3]; };
-    auto or_byte = [&](uint32_t A, uint32_t x) { atomicOr(&img[A >> 2], x << (8u * (A & 3u))); };
     uint32_t rem = my;
     if (P.raw)
     {
         // 0xFF, xn raw LE words, xn position bytes (p4_scalar_internal.cpp:163-197)
         if (t == 0)
-            or_byte(v0, 0xFFu);
+            ib[v0] = 0xFFu;
         const uint32_t pbase = v0 + 1u + 4u * P.xn;
 #pragma unroll
         for (uint32_t i = 0; i < 4u; ++i)
-            if (i < mc)
+            if (i < mc && rem != 0u)
             {
-                const bool on = rem != 0u;
-                const uint32_t j = on ? static_cast<uint32_t>(__builtin_ctz(rem)) : 0u;
+                const uint32_t j = static_cast<uint32_t>(__builtin_ctz(rem));
                 rem &= rem - 1u;
-                const uint32_t k = before + (on ? i : 0u);
-                const uint32_t A = v0 + 1u + 4u * k, q = A >> 2, sh = 8u * (A & 3u), x = on ? pick(j) : 0u;
-                atomicOr(&img[q], x << sh);
-                atomicOr(&img[q + 1u], sh ? x >> (32u - sh) : 0u);
-                or_byte(pbase + k, on ? 4u * t + j : 0u);
+                const uint32_t k = before + i, A = v0 + 1u + 4u * k, x = pick(j);
+                ib[A] = static_cast<uint8_t>(x);
+                ib[A + 1u] = static_cast<uint8_t>(x >> 8);
+                ib[A + 2u] = static_cast<uint8_t>(x >> 16);
+                ib[A + 3u] = static_cast<uint8_t>(x >> 24);
+                ib[pbase + k] = static_cast<uint8_t>(4u * t + j);
             }
         return sb;
     }
@@ -413,26 +414,28 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
     const uint32_t pbase = v0 + vtotal;
 #pragma unroll
     for (uint32_t i = 0; i < 4u; ++i)
-        if (i < mc)
+        if (i < mc && rem != 0u)
         {
-            const bool on = rem != 0u;
-            const uint32_t j = on ? static_cast<uint32_t>(__builtin_ctz(rem)) : 0u;
+            const uint32_t j = static_cast<uint32_t>(__builtin_ctz(rem));
             rem &= rem - 1u;
             const uint32_t x = pick(j);
             const uint32_t d2 = x - 156u, d3 = x - 16540u;
-            const uint32_t L = on ? vblen32(x) : 0u;
-            // the value's bytes as (hi:lo), zero above its length
+            const uint32_t L = vblen32(x);
+            // the value's first four bytes (the fifth, of a 5-byte value, is x >> 24)
             const uint32_t lo = L == 1u ? x
                               : L == 2u ? (0x9Cu + (d2 >> 8)) | ((d2 & 0xFFu) << 8)
                               : L == 3u ? (0xDCu + (d3 >> 16)) | ((d3 & 0xFFFFu) << 8)
-                              : L == 4u ? 0xFCu | (x << 8)
-                              : L == 5u ? 0xFDu | (x << 8) : 0u;
-            const uint32_t hi = L == 5u ? x >> 24 : 0u;
-            const uint32_t q = A >> 2, sh = 8u * (A & 3u);
-            atomicOr(&img[q], lo << sh);
-            atomicOr(&img[q + 1u], sh ? __builtin_amdgcn_alignbit(hi, lo, 32u - sh) : hi);
-            atomicOr(&img[q + 2u], sh ? hi >> (32u - sh) : 0u);
-            or_byte(pbase + before + (on ? i : 0u), on ? 4u * t + j : 0u);
+                              : (L == 4u ? 0xFCu : 0xFDu) | (x << 8);
+            ib[A] = static_cast<uint8_t>(lo);
+            if (L > 1u)
+                ib[A + 1u] = static_cast<uint8_t>(lo >> 8);
+            if (L > 2u)
+                ib[A + 2u] = static_cast<uint8_t>(lo >> 16);
+            if (L > 3u)
+                ib[A + 3u] = static_cast<uint8_t>(lo >> 24);
+            if (L > 4u)
+                ib[A + 4u] = static_cast<uint8_t>(x >> 24);
+            ib[pbase + before + i] = static_cast<uint8_t>(4u * t + j);
             A += L;
         }
     return sb;
