@@ -55,8 +55,8 @@ for f in glob.glob(sys.argv[1] + '/**/*kernel_stats.csv', recursive=True):
         for lib in ${LIBS:-tree}; do
           if [ $lib = tree ]; then unset TPF_LIB; else export TPF_LIB=$R/$lib; fi
           n=$(basename $lib .so)
-          timeout -k 10 240 python bench.py --workload $wl --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --no-probes ${BARGS} > $O/${T}_ab_${n}_$i.json 2> $O/${T}_ab_${n}_$i.err || fail "ab $n" $? $O/${T}_ab_${n}_$i.err 5
-          python -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['config']; r=d['roofline']; print(sys.argv[2], d['value'], 'ms', r.get('kernel_ms_avg'), 'verified', c.get('verified'), {k: v for k, v in c.items() if k.endswith('per_s')})" $O/${T}_ab_${n}_$i.json $n
+          timeout -k 10 240 python bench.py --workload $wl --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --no-probes ${BARGS} > $O/${T}_ab_${wl}_${n}_$i.json 2> $O/${T}_ab_${wl}_${n}_$i.err || fail "ab $n" $? $O/${T}_ab_${wl}_${n}_$i.err 5
+          python -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['config']; r=d['roofline']; print(sys.argv[3], sys.argv[2], d['value'], 'ms', r.get('kernel_ms_avg'), 'verified', c.get('verified'), {k: v for k, v in c.items() if k.endswith('per_s')})" $O/${T}_ab_${wl}_${n}_$i.json $n $wl
         done
       done ;;
     libs)
