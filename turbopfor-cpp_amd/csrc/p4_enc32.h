@@ -369,12 +369,12 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
     // Exception emission (round 4): the lane's i-th flagged value is taken
     // from its flag mask (lowest set bit, cleared after use), its byte address
     // is its rank (raw: 4 bytes each) or a wave scan of the vbyte lengths, and
-    // only the lanes that hold an i-th exception store its bytes -- plain LDS
-    // byte stores (every byte of the exception area has exactly one writer and
-    // the base payload ends before v0), no atomics and no per-length branches
-    // around the value arithmetic.  A round-4 variant that let every lane OR a
-    // zero into the image (no exec sections) was 27% slower on C3: the idle
-    // lanes' atomics hit the dword of the lane next to them.
+    // its bytes go out as plain LDS byte stores (every byte of the exception
+    // area has exactly one writer and the base payload ends before v0), no
+    // atomics.  A first round-4 form that let idle lanes OR zeros into the
+    // image was 27% slower on C3 (their atomics hit the dword of the lane next
+    // to them); byte stores under exec masks were level with the serial
+    // emission; the form below is 1.5% faster on C3.
     // the most exceptions any lane holds (wave-uniform loop bound)
     const uint32_t mc = __builtin_amdgcn_ballot_w64(cnt >= 4u) ? 4u
                         : __builtin_amdgcn_ballot_w64(cnt >= 3u) ? 3u
@@ -382,6 +382,14 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
                         : __builtin_amdgcn_ballot_w64(cnt >= 1u) ? 1u : 0u;
     auto pick = [&](uint32_t j) { return j == 0u ? ex[0] : j == 1u ? ex[1] : j == 2u ? ex[2] : ex[3]; };
     uint32_t rem = my;
+    // Every lane stores in every step: bytes a lane does not own that step
+    // (no i-th exception, or past the value's length) go to the lane's own
+    // dword of the staging area `val`, free once pack_base_runs has read it,
+    // so the steps carry no exec-mask sections and their SALU bookkeeping.
+    uint8_t * const trash = reinterpret_cast<uint8_t *>(val + t);
+    auto put = [&](bool own, uint32_t at, uint32_t k, uint32_t byte) {
+        *(own ? ib + at : trash + k) = static_cast<uint8_t>(byte);
+    };
     if (P.raw)
     {
         // 0xFF, xn raw LE words, xn position bytes (p4_scalar_internal.cpp:163-197)
@@ -390,16 +398,17 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
         const uint32_t pbase = v0 + 1u + 4u * P.xn;
 #pragma unroll
         for (uint32_t i = 0; i < 4u; ++i)
-            if (i < mc && rem != 0u)
+            if (i < mc)
             {
-                const uint32_t j = static_cast<uint32_t>(__builtin_ctz(rem));
+                const bool on = rem != 0u;
+                const uint32_t j = on ? static_cast<uint32_t>(__builtin_ctz(rem)) : 0u;
                 rem &= rem - 1u;
                 const uint32_t k = before + i, A = v0 + 1u + 4u * k, x = pick(j);
-                ib[A] = static_cast<uint8_t>(x);
-                ib[A + 1u] = static_cast<uint8_t>(x >> 8);
-                ib[A + 2u] = static_cast<uint8_t>(x >> 16);
-                ib[A + 3u] = static_cast<uint8_t>(x >> 24);
-                ib[pbase + k] = static_cast<uint8_t>(4u * t + j);
+                put(on, A, 0u, x);
+                put(on, A + 1u, 1u, x >> 8);
+                put(on, A + 2u, 2u, x >> 16);
+                put(on, A + 3u, 3u, x >> 24);
+                put(on, pbase + k, 0u, 4u * t + j);
             }
         return sb;
     }
@@ -414,9 +423,10 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
     const uint32_t pbase = v0 + vtotal;
 #pragma unroll
     for (uint32_t i = 0; i < 4u; ++i)
-        if (i < mc && rem != 0u)
+        if (i < mc)
         {
-            const uint32_t j = static_cast<uint32_t>(__builtin_ctz(rem));
+            const bool on = rem != 0u;
+            const uint32_t j = on ? static_cast<uint32_t>(__builtin_ctz(rem)) : 0u;
             rem &= rem - 1u;
             const uint32_t x = pick(j);
             const uint32_t d2 = x - 156u, d3 = x - 16540u;
@@ -426,17 +436,13 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
                               : L == 2u ? (0x9Cu + (d2 >> 8)) | ((d2 & 0xFFu) << 8)
                               : L == 3u ? (0xDCu + (d3 >> 16)) | ((d3 & 0xFFFFu) << 8)
                               : (L == 4u ? 0xFCu : 0xFDu) | (x << 8);
-            ib[A] = static_cast<uint8_t>(lo);
-            if (L > 1u)
-                ib[A + 1u] = static_cast<uint8_t>(lo >> 8);
-            if (L > 2u)
-                ib[A + 2u] = static_cast<uint8_t>(lo >> 16);
-            if (L > 3u)
-                ib[A + 3u] = static_cast<uint8_t>(lo >> 24);
-            if (L > 4u)
-                ib[A + 4u] = static_cast<uint8_t>(x >> 24);
-            ib[pbase + before + i] = static_cast<uint8_t>(4u * t + j);
-            A += L;
+            put(on, A, 0u, lo);
+            put(on && L > 1u, A + 1u, 1u, lo >> 8);
+            put(on && L > 2u, A + 2u, 2u, lo >> 16);
+            put(on && L > 3u, A + 3u, 3u, lo >> 24);
+            put(on && L > 4u, A + 4u, 0u, x >> 24);
+            put(on, pbase + before + i, 1u, 4u * t + j);
+            A += on ? L : 0u;
         }
     return sb;
 }
