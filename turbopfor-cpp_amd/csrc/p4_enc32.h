@@ -36,7 +36,8 @@ __device__ __forceinline__ uint32_t bw32(uint32_t x) { return x ? 32u - __builti
 // vbPut32 byte length (p4_scalar_internal.cpp:47-89)
 __device__ __forceinline__ uint32_t vblen32(uint32_t x)
 {
-    return x < 156u ? 1u : x < 16540u ? 2u : x < 2113692u ? 3u : x <= 0xFFFFFFu ? 4u : 5u;
+    // a sum of compares, not a ?: chain (which compiled into exec-mask branches)
+    return 1u + (x >= 156u) + (x >= 16540u) + (x >= 2113692u) + (x > 0xFFFFFFu);
 }
 
 #ifndef TPF_PLAN_FFBH
@@ -372,19 +373,23 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
     // to them); byte stores under exec masks were level with the serial
     // emission; the form below is 1.5% faster on C3.
     // the most exceptions any lane holds (wave-uniform loop bound)
-    const uint32_t mc = __builtin_amdgcn_ballot_w64(cnt >= 4u) ? 4u
-                        : __builtin_amdgcn_ballot_w64(cnt >= 3u) ? 3u
-                        : __builtin_amdgcn_ballot_w64(cnt >= 2u) ? 2u
-                        : __builtin_amdgcn_ballot_w64(cnt >= 1u) ? 1u : 0u;
-    auto pick = [&](uint32_t j) { return j == 0u ? ex[0] : j == 1u ? ex[1] : j == 2u ? ex[2] : ex[3]; };
+    const uint32_t mc = (__builtin_amdgcn_ballot_w64(cnt >= 1u) != 0u) + (__builtin_amdgcn_ballot_w64(cnt >= 2u) != 0u) +
+                        (__builtin_amdgcn_ballot_w64(cnt >= 3u) != 0u) + (__builtin_amdgcn_ballot_w64(cnt >= 4u) != 0u);
+    // ex[j] for a per-lane j as two levels of selects (a four-way ?: chain
+    // was compiled into exec-mask branches)
+    auto pick = [&](uint32_t j) {
+        const uint32_t e01 = (j & 1u) ? ex[1] : ex[0], e23 = (j & 1u) ? ex[3] : ex[2];
+        return (j & 2u) ? e23 : e01;
+    };
     uint32_t rem = my;
     // Every lane stores in every step: bytes a lane does not own that step
     // (no i-th exception, or past the value's length) go to the lane's own
     // dword of the staging area `val`, free once pack_base_runs has read it,
     // so the steps carry no exec-mask sections and their SALU bookkeeping.
     uint8_t * const trash = reinterpret_cast<uint8_t *>(val + t);
+    const uint32_t trash_at = static_cast<uint32_t>(trash - ib); // (mod 2^32: LDS addresses are 32-bit)
     auto put = [&](bool own, uint32_t at, uint32_t k, uint32_t byte) {
-        *(own ? ib + at : trash + k) = static_cast<uint8_t>(byte);
+        ib[__builtin_unpredictable(own) ? at : trash_at + k] = static_cast<uint8_t>(byte);
     };
     if (P.raw)
     {
@@ -412,7 +417,7 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
     uint32_t mylen = 0u;
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j)
-        mylen += ((my >> j) & 1u) ? vblen32(ex[j]) : 0u;
+        mylen += vblen32(ex[j]) & (0u - ((my >> j) & 1u));
     const uint32_t lincl = wave_incl_scan(mylen);
     const uint32_t vtotal = __builtin_amdgcn_readlane(lincl, 63);
     uint32_t A = v0 + lincl - mylen;
@@ -426,12 +431,17 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
             rem &= rem - 1u;
             const uint32_t x = pick(j);
             const uint32_t d2 = x - 156u, d3 = x - 16540u;
-            const uint32_t L = vblen32(x);
-            // the value's first four bytes (the fifth, of a 5-byte value, is x >> 24)
-            const uint32_t lo = L == 1u ? x
-                              : L == 2u ? (0x9Cu + (d2 >> 8)) | ((d2 & 0xFFu) << 8)
-                              : L == 3u ? (0xDCu + (d3 >> 16)) | ((d3 & 0xFFFFu) << 8)
-                              : (L == 4u ? 0xFCu : 0xFDu) | (x << 8);
+            const bool g1 = x >= 156u, g2 = x >= 16540u, g3 = x >= 2113692u, g4 = x > 0xFFFFFFu;
+            const uint32_t L = 1u + g1 + g2 + g3 + g4;
+            // the value's first four bytes (the fifth, of a 5-byte value, is
+            // x >> 24), selected by the range tests (an L == k chain compiled
+            // into exec-mask branches)
+            const uint32_t c2 = (0x9Cu + (d2 >> 8)) | ((d2 & 0xFFu) << 8);
+            const uint32_t c3 = (0xDCu + (d3 >> 16)) | ((d3 & 0xFFFFu) << 8);
+            const uint32_t c45 = (g4 ? 0xFDu : 0xFCu) | (x << 8);
+            const uint32_t c23 = __builtin_unpredictable(g2) ? c3 : c2;
+            const uint32_t c25 = __builtin_unpredictable(g3) ? c45 : c23;
+            const uint32_t lo = __builtin_unpredictable(g1) ? c25 : x;
             put(on, A, 0u, lo);
             put(on && L > 1u, A + 1u, 1u, lo >> 8);
             put(on && L > 2u, A + 2u, 2u, lo >> 16);
@@ -496,7 +506,7 @@ __device__ __forceinline__ void copy_out_image16(const uint32_t * img, uint32_t 
         }
         const uint32_t last = (end - 1u) >> 4; // chunk holding the block's last byte
         const uint32_t k = t < 16u ? 0u : last;
-        const bool edge = t < 16u ? first_partial : (t < 32u && last > 0u && (end & 15u) != 0u);
+        const bool edge = ((t < 16u) & first_partial) | ((t >= 16u) & (t < 32u) & (last > 0u) & ((end & 15u) != 0u));
         const uint32_t gi = 16u * k + (t & 15u); // byte index from a16
         if (edge && gi >= ph && gi < end)
             a16[gi] = ib[base + gi];
