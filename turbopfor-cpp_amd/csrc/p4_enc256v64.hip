@@ -77,66 +77,27 @@ __device__ __forceinline__ PlanG plan_block128v64(uint64_t x0, uint64_t x1, uint
     return plan_block_g<Fmt::V128X64>(v, 128u, hist, t);
 }
 
-// OR cnt (0..2) consecutive nb-bit (<= 64) values a, b into the image's bit
-// stream at `bit` (five dwords at most).
-__device__ __forceinline__ void or_pair64(uint32_t * img, uint32_t bit, uint64_t a, uint64_t b, uint32_t cnt, uint32_t nb)
+// OR a lane's one or two consecutive nb-bit values a, b (b = 0 for one;
+// both < 2^nb, 1 <= nb <= 64) into the image's bit stream at `bit` (five
+// dwords at most).  No branches (round 4, as or_run in p4_enc32.h): the pair
+// as 128 bits (b shifted by nb in two steps so that 64 shifts it out), the
+// lane's bit offset applied with 64-bit shifts, a wave-uniform store bound.
+__device__ __forceinline__ void or_pair64(uint32_t * img, uint32_t bit, uint64_t a, uint64_t b, uint32_t nb)
 {
-    if (cnt == 0u || nb == 0u)
-        return;
-    const uint64_t m = mask64d(nb);
-    a &= m;
-    b = cnt > 1u ? (b & m) : 0ull;
-    const uint64_t lo = a | shl64(b, nb);
-    const uint64_t hi = nb == 0u ? 0ull : (nb >= 64u ? b : (b >> (64u - nb)));
+    const uint64_t lo = a | ((b << (nb - 1u)) << 1);
+    const uint64_t hi = b >> (64u - nb);
     const uint32_t sh = bit & 31u, q = bit >> 5;
-    const uint32_t d0 = static_cast<uint32_t>(lo), d1 = static_cast<uint32_t>(lo >> 32);
-    const uint32_t d2 = static_cast<uint32_t>(hi), d3 = static_cast<uint32_t>(hi >> 32);
     uint32_t w[5];
-    w[0] = d0 << sh;
-    w[1] = sh ? __builtin_amdgcn_alignbit(d1, d0, 32u - sh) : d1;
-    w[2] = sh ? __builtin_amdgcn_alignbit(d2, d1, 32u - sh) : d2;
-    w[3] = sh ? __builtin_amdgcn_alignbit(d3, d2, 32u - sh) : d3;
-    w[4] = sh ? (d3 >> (32u - sh)) : 0u;
-    const uint32_t nw = (sh + cnt * nb + 31u) >> 5;
+    w[0] = static_cast<uint32_t>(lo) << sh;
+    w[1] = static_cast<uint32_t>((lo << sh) >> 32);
+    w[2] = static_cast<uint32_t>((((hi << 32) | (lo >> 32)) << sh) >> 32);
+    w[3] = static_cast<uint32_t>((hi << sh) >> 32);
+    w[4] = static_cast<uint32_t>(((hi >> 32) << sh) >> 32);
+    const uint32_t maxw = (62u + 2u * nb) >> 5;
 #pragma unroll
     for (uint32_t i = 0; i < 5; ++i)
-        if (i < nw && w[i] != 0u)
+        if (i < maxw)
             atomicOr(&img[q + i], w[i]);
-}
-
-// Interleave the low 16 bits of x to the even bit positions of a dword.
-__device__ __forceinline__ uint32_t spread16(uint32_t x)
-{
-    x &= 0xFFFFu;
-    x = (x | (x << 8)) & 0x00FF00FFu;
-    x = (x | (x << 4)) & 0x0F0F0F0Fu;
-    x = (x | (x << 2)) & 0x33333333u;
-    x = (x | (x << 1)) & 0x55555555u;
-    return x;
-}
-
-// vbPut64 encoding (p4_scalar_internal.cpp:447-476) of x at image byte pos.
-__device__ __forceinline__ void vbput64_img(uint32_t * img, uint32_t pos, uint64_t x)
-{
-    const uint32_t bp = pos * 8u;
-    if (x < 152u)
-        or_bits(img, bp, static_cast<uint32_t>(x), 8);
-    else if (x < 16536u)
-    {
-        const uint32_t d = static_cast<uint32_t>(x) - 152u;
-        or_bits(img, bp, (0x98u + (d >> 8)) | ((d & 0xFFu) << 8), 16);
-    }
-    else if (x < 2113688u)
-    {
-        const uint32_t d = static_cast<uint32_t>(x) - 16536u;
-        or_bits(img, bp, (0xD8u + (d >> 16)) | ((d & 0xFFFFu) << 8), 24);
-    }
-    else
-    {
-        const uint32_t nb = (bw64d(x) + 7u) >> 3;
-        or_bits(img, bp, 0xF8u + (nb - 3u), 8);
-        or_bits64(img, bp + 8u, x, 8u * nb);
-    }
 }
 
 // Build one 128v64 block (p4Enc128v64 = writeHeader64 + p4Enc128v64Payload)
@@ -201,7 +162,7 @@ __device__ __forceinline__ uint32_t emit_block128v64(uint32_t * img, uint32_t * 
     else if (b > 32u)
     {
         // horizontal 64-bit stream: values 2t, 2t+1 are consecutive
-        or_pair64(img, pw * 32u + 2u * t * b, m0, m1, 2u, b);
+        or_pair64(img, pw * 32u + 2u * t * b, m0, m1, b);
     }
     if (P.bx == 0u)
         return sb;
@@ -209,50 +170,72 @@ __device__ __forceinline__ uint32_t emit_block128v64(uint32_t * img, uint32_t * 
     const uint32_t cnt = f0 + f1;
     const uint32_t before = static_cast<uint32_t>(__builtin_popcountll(B0 & lanemask_lt()) + __builtin_popcountll(B1 & lanemask_lt()));
     const uint64_t e0 = b >= 64u ? 0ull : (x0 >> b), e1 = b >= 64u ? 0ull : (x1 >> b);
-    const uint64_t xa = f0 ? e0 : e1; // this lane's exceptions, compacted
+    // Exception bytes go out as plain byte stores from every lane in every
+    // step: bytes a lane does not own go to its own 8 scratch bytes in `val`
+    // (free once the base payload is packed), so the steps carry no
+    // exec-mask sections (round 4, as emit_block256).
+    const uint32_t trash_at = static_cast<uint32_t>(reinterpret_cast<uint8_t *>(val + 2u * t) - ib);
+    auto put = [&](bool own, uint32_t at, uint32_t k, uint32_t byte) {
+        ib[__builtin_unpredictable(own) ? at : trash_at + (k & 7u)] = static_cast<uint8_t>(byte);
+    };
     if (P.bx <= 64u)
     {
-        // [0x80|b][bx][bitmap 16 B][xn * bx bits][base]
-        if (t < 4u)
+        // [0x80|b][bx][bitmap 16 B][xn * bx bits][base]: bitmap byte k holds
+        // elements 8k..8k+7, i.e. lanes 4k..4k+3 (x0 on even bits, x1 on odd)
+        if (t < 16u)
         {
-            const uint32_t piece = spread16(static_cast<uint32_t>(B0 >> (16u * t))) | (spread16(static_cast<uint32_t>(B1 >> (16u * t))) << 1);
-            or_bits(img, (sb + 2u) * 8u + 32u * t, piece, 32);
+            uint32_t n0 = static_cast<uint32_t>(B0 >> (4u * t)) & 15u, n1 = static_cast<uint32_t>(B1 >> (4u * t)) & 15u;
+            n0 = (n0 | (n0 << 2)) & 0x33u;
+            n0 = (n0 | (n0 << 1)) & 0x55u;
+            n1 = (n1 | (n1 << 2)) & 0x33u;
+            n1 = (n1 | (n1 << 1)) & 0x55u;
+            ib[sb + 2u + t] = static_cast<uint8_t>(n0 | (n1 << 1));
         }
-        or_pair64(img, (sb + 18u) * 8u + before * P.bx, xa, e1, cnt, P.bx);
+        const uint64_t mx = mask64d(P.bx);
+        if (cnt != 0u) // lanes without exceptions share `before` with a neighbour: no zero ORs
+            or_pair64(img, (sb + 18u) * 8u + before * P.bx, (f0 ? e0 : e1) & mx, cnt > 1u ? (e1 & mx) : 0ull, P.bx);
         return sb;
     }
     // vbyte: [0x40|b][xn][base 16b][V][positions]
     const uint32_t v0 = sb + 2u + 16u * b;
     if (P.raw)
     {
+        // 0xFF, xn raw LE u64, xn position bytes
         if (t == 0)
-            or_bits(img, v0 * 8u, 0xFFu, 8);
-        if (f0)
+            ib[v0] = 0xFFu;
+        const uint32_t a0 = v0 + 1u + 8u * before, a1 = a0 + 8u * f0;
+#pragma unroll
+        for (uint32_t k = 0; k < 8u; ++k)
         {
-            or_bits64(img, (v0 + 1u + 8u * before) * 8u, e0, 64);
-            or_bits(img, (v0 + 1u + 8u * P.xn + before) * 8u, 2u * t, 8);
+            put(f0, a0 + k, k, static_cast<uint32_t>(e0 >> (8u * k)));
+            put(f1, a1 + k, k, static_cast<uint32_t>(e1 >> (8u * k)));
         }
-        if (f1)
-        {
-            or_bits64(img, (v0 + 1u + 8u * (before + f0)) * 8u, e1, 64);
-            or_bits(img, (v0 + 1u + 8u * P.xn + before + f0) * 8u, 2u * t + 1u, 8);
-        }
+        const uint32_t pp = v0 + 1u + 8u * P.xn + before;
+        put(f0, pp, 0u, 2u * t);
+        put(f1, pp + f0, 1u, 2u * t + 1u);
         return sb;
     }
+    // vbPut64 (p4_scalar_internal.cpp:447-476): marker byte, then up to 8 bytes
     const uint32_t l0 = f0 ? vblen64(e0) : 0u, l1 = f1 ? vblen64(e1) : 0u;
     const uint32_t lincl = wave_incl_scan(l0 + l1);
     const uint32_t vtot = __builtin_amdgcn_readlane(lincl, 63);
     const uint32_t pos = v0 + lincl - l0 - l1;
-    if (f0)
-    {
-        vbput64_img(img, pos, e0);
-        or_bits(img, (v0 + vtot + before) * 8u, 2u * t, 8);
-    }
-    if (f1)
-    {
-        vbput64_img(img, pos + l0, e1);
-        or_bits(img, (v0 + vtot + before + f0) * 8u, 2u * t + 1u, 8);
-    }
+    auto vbput = [&](bool own, uint32_t at, uint64_t x, uint32_t L) {
+        const bool g1 = x >= 152u, g2 = x >= 16536u, g3 = x >= 2113688u;
+        const uint32_t d2 = static_cast<uint32_t>(x) - 152u, d3 = static_cast<uint32_t>(x) - 16536u;
+        const uint32_t mk3 = 0xF8u + (L - 1u) - 3u;
+        const uint32_t mk12 = __builtin_unpredictable(g2) ? 0xD8u + (d3 >> 16) : 0x98u + (d2 >> 8);
+        const uint32_t mk = __builtin_unpredictable(g3) ? mk3 : (__builtin_unpredictable(g1) ? mk12 : static_cast<uint32_t>(x));
+        const uint64_t tail = __builtin_unpredictable(g3) ? x : (__builtin_unpredictable(g2) ? (d3 & 0xFFFFu) : (d2 & 0xFFu));
+        put(own, at, 0u, mk);
+#pragma unroll
+        for (uint32_t k = 1; k < 9u; ++k)
+            put(own && k < L, at + k, k, static_cast<uint32_t>(tail >> (8u * (k - 1u))));
+    };
+    vbput(f0, pos, e0, l0);
+    vbput(f1, pos + l0, e1, l1);
+    put(f0, v0 + vtot + before, 0u, 2u * t);
+    put(f1, v0 + vtot + before + f0, 1u, 2u * t + 1u);
     return sb;
 }
 

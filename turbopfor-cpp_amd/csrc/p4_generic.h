@@ -394,7 +394,9 @@ __device__ __forceinline__ uint32_t bw64d(uint64_t x) { return x ? 64u - static_
 // vbPut64 byte length (p4_scalar_internal.cpp:447-476)
 __device__ __forceinline__ uint32_t vblen64(uint64_t x)
 {
-    return x < 152u ? 1u : x < 16536u ? 2u : x < 2113688u ? 3u : 1u + ((bw64d(x) + 7u) >> 3);
+    // selects on the range tests, not a ?: chain (which compiled into exec-mask branches)
+    const uint32_t small = 1u + (x >= 152u) + (x >= 16536u);
+    return __builtin_unpredictable(x >= 2113688u) ? 1u + ((bw64d(x) + 7u) >> 3) : small;
 }
 
 __device__ __forceinline__ uint64_t wave_or64(uint64_t x)
