@@ -57,9 +57,8 @@ constexpr uint32_t kEncNCWrite = TPF_ENC_NC_WRITE;
 // deltaEnc1 (p4_scalar_internal.h:711-719): d[i] = in[i] - in[i-1] - 1, in[-1] = start.
 __device__ __forceinline__ u32x4 delta_encode(const u32x4 & v, uint32_t start, uint32_t t)
 {
-    uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(v.w), 1, 64));
-    if (t == 0)
-        prev = start;
+    const uint32_t prev = wave_shr1(v.w, start);
+    (void)t;
     return u32x4{v.x - prev - 1u, v.y - v.x - 1u, v.z - v.y - 1u, v.w - v.z - 1u};
 }
 

@@ -37,21 +37,14 @@ __device__ __forceinline__ void split2(const u32x4 & c, uint64_t & x0, uint64_t 
     x1 = (static_cast<uint64_t>(c.w) << 32) | c.z;
 }
 
-// 64-bit lane shuffle up by one (ds_bpermute twice)
-__device__ __forceinline__ uint64_t shfl_up1_64(uint64_t x)
-{
-    const uint32_t lo = static_cast<uint32_t>(__shfl_up(static_cast<int>(static_cast<uint32_t>(x)), 1, 64));
-    const uint32_t hi = static_cast<uint32_t>(__shfl_up(static_cast<int>(static_cast<uint32_t>(x >> 32)), 1, 64));
-    return (static_cast<uint64_t>(hi) << 32) | lo;
-}
-
 // deltaEnc1 (p4_scalar_internal.h:711-719) over one 128-value block:
 // d[e] = x[e] - x[e-1] - 1 with x[-1] = prev.
 __device__ __forceinline__ void delta_encode64(uint64_t & x0, uint64_t & x1, uint64_t prev, uint32_t t)
 {
-    uint64_t p = shfl_up1_64(x1);
-    if (t == 0)
-        p = prev;
+    // x1 of lane t-1, lane 0: prev (two DPP wave_shr:1, no ds_bpermute)
+    const uint64_t p = (static_cast<uint64_t>(wave_shr1(static_cast<uint32_t>(x1 >> 32), static_cast<uint32_t>(prev >> 32))) << 32) |
+                       wave_shr1(static_cast<uint32_t>(x1), static_cast<uint32_t>(prev));
+    (void)t;
     const uint64_t d0 = x0 - p - 1u, d1 = x1 - x0 - 1u;
     x0 = d0;
     x1 = d1;

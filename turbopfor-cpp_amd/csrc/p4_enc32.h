@@ -328,7 +328,7 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
     if (P.bx <= 32u)
     {
         // [0x80|b][bx][bitmap 32B][xn*bx bits horizontal][256v32 base]
-        const uint32_t mynext = static_cast<uint32_t>(__shfl_down(static_cast<int>(my), 1, 64));
+        const uint32_t mynext = wave_shl1(my, 0u);
         if (t == 0)
         {
             ib[sb] = static_cast<uint8_t>(0x80u | b);

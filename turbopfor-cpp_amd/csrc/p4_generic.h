@@ -357,17 +357,16 @@ __device__ __forceinline__ void delta_enc_g(T v[4], T prev0, uint32_t n, uint32_
         T prev;
         if constexpr (sizeof(T) == 8)
         {
-            const uint32_t lo = static_cast<uint32_t>(__shfl_up(static_cast<int>(static_cast<uint32_t>(v[j])), 1, 64));
-            const uint32_t hi = static_cast<uint32_t>(__shfl_up(static_cast<int>(static_cast<uint32_t>(v[j] >> 32)), 1, 64));
+            // lane t-1's value by DPP wave_shr:1 (lane 0: the previous row's last)
+            const uint64_t p0 = j == 0 ? static_cast<uint64_t>(prev0) : readlane_u64(v[j - 1], 63);
+            const uint32_t lo = wave_shr1(static_cast<uint32_t>(v[j]), static_cast<uint32_t>(p0));
+            const uint32_t hi = wave_shr1(static_cast<uint32_t>(v[j] >> 32), static_cast<uint32_t>(p0 >> 32));
             prev = (static_cast<uint64_t>(hi) << 32) | lo;
-            if (t == 0)
-                prev = j == 0 ? prev0 : readlane_u64(v[j - 1], 63);
         }
         else
         {
-            prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(v[j]), 1, 64));
-            if (t == 0)
-                prev = j == 0 ? prev0 : __builtin_amdgcn_readlane(v[j - 1], 63);
+            const uint32_t p0 = j == 0 ? static_cast<uint32_t>(prev0) : __builtin_amdgcn_readlane(v[j - 1], 63);
+            prev = wave_shr1(static_cast<uint32_t>(v[j]), p0);
         }
         d[j] = (t + 64u * j < n) ? T(v[j] - prev - 1u) : T(0);
     }

@@ -101,6 +101,18 @@ __device__ __forceinline__ uint32_t lds_bits(const uint32_t * w, uint32_t bp, ui
     return __builtin_amdgcn_alignbit(w[q + 1], w[q], bp & 31u) & mask32(nb);
 }
 
+// Lane t gets x of lane t-1, lane 0 gets `first` (DPP wave_shr:1, one VALU
+// op; __shfl_up is a ds_bpermute through the LDS pipe).  Round 4.
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t x, uint32_t first)
+{
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(first), static_cast<int>(x), 0x138, 0xf, 0xf, false));
+}
+// Lane t gets x of lane t+1, lane 63 gets `last` (DPP wave_shl:1).
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t x, uint32_t last)
+{
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(last), static_cast<int>(x), 0x130, 0xf, 0xf, false));
+}
+
 // ---- wave64 inclusive scan (DPP row_shr + row_bcast, gfx9 idiom) ----------
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
 {
