@@ -95,10 +95,10 @@ void tc(int rc)
 }
 
 // Can the copy engines (and, mapped, the kernels) use the host range
-// [p, p + bytes) as it is?  Yes when HIP knows it as ONE allocation or
-// registration: hipHostMalloc'd or caller-registered host memory (`d` = its
-// device address) or device memory.  A pageable range -- or one that only
-// shares a page with someone else's registration -- is STAGED: host threads
+// [p, p + bytes) as it is?  Yes when HIP knows both its ends as page-locked
+// host memory (hipHostMalloc'd or caller-registered; `d` = its device
+// address) or as device memory.  A pageable range -- or one whose far end
+// lies outside any registration -- is STAGED: host threads
 // copy it into / out of the pipeline's pinned buffers.  The library never
 // page-locks caller memory.  (Until round 3 it did, hipHostRegister for the
 // length of a call: a call's registration and release of pageable pages that
@@ -108,7 +108,11 @@ void tc(int rc)
 struct Reach
 {
     bool direct = true;
+    bool dev = false; // device (or managed) memory handed over as a host pointer
     void * d = nullptr;
+    // copy kinds for a direct range (explicit rather than hipMemcpyDefault)
+    hipMemcpyKind up() const { return dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice; }
+    hipMemcpyKind down() const { return dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost; }
 };
 
 bool lookup(const void * q, hipPointerAttribute_t & a)
@@ -133,14 +137,20 @@ Reach reach(const void * ptr, size_t bytes)
         r.direct = false;
         return r;
     }
-    if (a.type == hipMemoryTypeHost && b.type == hipMemoryTypeHost && a.hostPointer && a.hostPointer == b.hostPointer)
+    if (a.type == hipMemoryTypeHost && b.type == hipMemoryTypeHost)
     {
-        if (a.devicePointer)
+        // both ends page-locked.  (Not "one hostPointer": for an interior
+        // pointer -- torch's pinned caching allocator hands those out -- HIP
+        // reports the queried address, so that test sent every pinned torch
+        // buffer through the pageable staging: host encode 12.9 -> 9.8 G
+        // int32/s, decode 12.3 -> 10.9, round 4.)
+        if (a.devicePointer && a.hostPointer)
             r.d = static_cast<uint8_t *>(a.devicePointer) + (lo - static_cast<const uint8_t *>(a.hostPointer));
         return r;
     }
     // device (or managed) memory handed over as a host pointer: the copy engines take it as it is
     r.direct = (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) && a.type == b.type;
+    r.dev = r.direct;
     return r;
 }
 
@@ -432,7 +442,7 @@ int host_dec_impl(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64
                 src_in = s;
             }
             hc(hipMemcpyAsync(d_off, st_off, (nb + 1) * 8, hipMemcpyHostToDevice, P.cs), "H2D off");
-            hc(hipMemcpyAsync(d_in, src_in, bytes, hipMemcpyDefault, P.cs), "H2D bytes");
+            hc(hipMemcpyAsync(d_in, src_in, bytes, r_in.direct ? r_in.up() : hipMemcpyHostToDevice, P.cs), "H2D bytes");
             if (h_starts)
             {
                 const void * src_st = static_cast<const uint8_t *>(h_starts) + c0 * es;
@@ -442,7 +452,7 @@ int host_dec_impl(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64
                     std::memcpy(s, src_st, nb * es);
                     src_st = s;
                 }
-                hc(hipMemcpyAsync(d_start, src_st, nb * es, hipMemcpyDefault, P.cs), "H2D starts");
+                hc(hipMemcpyAsync(d_start, src_st, nb * es, r_st.direct ? r_st.up() : hipMemcpyHostToDevice, P.cs), "H2D starts");
             }
             hc(hipEventRecord(sl.up, P.cs), "record up");
             hc(hipStreamWaitEvent(P.ks, sl.up, 0), "wait up");
@@ -451,7 +461,7 @@ int host_dec_impl(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64
             {
                 uint8_t * dst = static_cast<uint8_t *>(h_vals) + c0 * uv * es;
                 if (r_vals.direct)
-                    hc(hipMemcpyAsync(dst, out, nb * uv * es, hipMemcpyDefault, P.ks), "D2H vals");
+                    hc(hipMemcpyAsync(dst, out, nb * uv * es, r_vals.down(), P.ks), "D2H vals");
                 else
                 {
                     void * s = sl.hout.get(chunk * uv * es);
@@ -618,7 +628,7 @@ int tpf_host_enc(int fmt, const void * h_vals, uint64_t nblocks, unsigned n, int
             if (dout)
                 tc(tpf_copy_async(dout + pos, sl.in.p, total, P.ks));
             else if (r_out.direct)
-                hc(hipMemcpyAsync(h_out + pos, sl.in.p, total, hipMemcpyDefault, P.ks), "D2H bytes");
+                hc(hipMemcpyAsync(h_out + pos, sl.in.p, total, r_out.down(), P.ks), "D2H bytes");
             else
             {
                 void * st = sl.hout.get(cap);
@@ -647,7 +657,7 @@ int tpf_host_enc(int fmt, const void * h_vals, uint64_t nblocks, unsigned n, int
                 par_copy(st, src_vals, nb * uv * es);
                 src_vals = st;
             }
-            hc(hipMemcpyAsync(d_vals, src_vals, nb * uv * es, hipMemcpyDefault, P.cs), "H2D vals");
+            hc(hipMemcpyAsync(d_vals, src_vals, nb * uv * es, r_vals.direct ? r_vals.up() : hipMemcpyHostToDevice, P.cs), "H2D vals");
             const void * dstart = nullptr;
             uint64_t s0 = start0;
             if (d1 && h_starts)
@@ -660,7 +670,7 @@ int tpf_host_enc(int fmt, const void * h_vals, uint64_t nblocks, unsigned n, int
                     std::memcpy(st, src_st, nb * es);
                     src_st = st;
                 }
-                hc(hipMemcpyAsync(d_start, src_st, nb * es, hipMemcpyDefault, P.cs), "H2D starts");
+                hc(hipMemcpyAsync(d_start, src_st, nb * es, r_st.direct ? r_st.up() : hipMemcpyHostToDevice, P.cs), "H2D starts");
                 dstart = d_start;
             }
             else if (d1 && c0 > 0)
