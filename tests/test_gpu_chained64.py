@@ -138,3 +138,63 @@ def test_chained64_large_roundtrip():
     torch.cuda.synchronize()
     assert int(err.item()) == -1
     assert torch.equal(out, vals)
+
+
+def _vb64_positions(blk):
+    """Byte range of the position list of a vbyte-mode 128v64 block (None if
+    the block is not in vbyte mode): [0x40|b][xn][16 b base bytes][values][xn
+    positions]; values are 0xFF + 8 xn raw words or xn vbyte64 values
+    (markers < 0x98: 1 byte, < 0xD8: 2, < 0xF8: 3, else marker - 0xF8 + 4)."""
+    h = blk[0]
+    if h & 0xC0 != 0x40:
+        return None
+    b = h & 0x3F
+    b = 64 if b == 63 else b
+    xn = blk[1]
+    c = 2 + 16 * b
+    if blk[c] == 0xFF:
+        c += 1 + 8 * xn
+    else:
+        for _ in range(xn):
+            m = blk[c]
+            c += 1 if m < 0x98 else 2 if m < 0xD8 else 3 if m < 0xF8 else m - 0xF8 + 4
+    return c, c + xn
+
+
+def test_chained64_repeated_positions():
+    """Units whose vbyte exception positions repeat (a position byte patched to
+    its predecessor's): the reference ORs the two exceptions into one element,
+    so the unit's delta total is not base + sum(ex) << b.  Phase A's lane path
+    must decline those units (p4_dsum64_lanes.h) and the wave decoder sum them
+    exactly; every later unit's start depends on it."""
+    fmt, nu, width, start0 = "256v64", 300, 256, 1 << 33
+    rng = np.random.default_rng(5)
+    gaps = rng.integers(0, 40, size=(nu, width)).astype(np.uint64)
+    exc = rng.random((nu, width)) < 0.05
+    gaps = np.where(exc, rng.integers(1 << 20, 1 << 30, size=(nu, width), dtype=np.uint64), gaps)
+    with np.errstate(over="ignore"):
+        vals = (np.cumsum(gaps.reshape(-1) + np.uint64(1), dtype=np.uint64) + np.uint64(start0)).reshape(nu, width)
+    starts = np.concatenate([np.array([start0], dtype=np.uint64), vals[:-1, -1]])
+    units = [bytearray(oracle_lib.encode(fmt, vals[i], d1=True, start=int(starts[i]))) for i in range(nu)]
+    patched = 0
+    for i in range(0, nu, 7):
+        u = units[i]
+        # the unit's first block: its length from a plain oracle decode of 128 values
+        _, l0 = oracle_lib.decode("128v64", bytes(u), 128, d1=True, start=0)
+        for off0, blk in ((0, u[:l0]), (l0, u[l0:])):
+            r = _vb64_positions(bytes(blk))
+            if r is not None and r[1] - r[0] >= 2:
+                u[off0 + r[0] + 1] = u[off0 + r[0]]
+                patched += 1
+                break
+    assert patched >= 10
+    packed_np = np.frombuffer(b"".join(bytes(u) for u in units), dtype=np.uint8)
+    offs_np = np.concatenate([[0], np.cumsum([len(u) for u in units])]).astype(np.int64)
+    exp = _oracle_sequential(fmt, packed_np, offs_np, nu, width, start0)
+    packed = torch.from_numpy(packed_np.copy()).to(DEV)
+    offs = torch.from_numpy(offs_np).to(DEV)
+    err = torch.zeros(1, dtype=torch.int64, device=DEV)
+    out = tpf.dec64_chained(fmt, packed, offs, nu, start0=start0, err=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == -1
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint64), exp)
