@@ -1043,7 +1043,7 @@ def run_c3chain64(args, world, rank, dev, T):
     value = nb * 256 * world / (elapsed / args.steps) / 1e9
     roof = {"bound": "hbm", "achieved": round(alg / (avg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), **traffic_fields("c3chain64", nb),
-            "kernel": "k_dec128v64w<2, Sum> + run scan (u64) + k_dec128v64w<2, Prefix>", "kernel_ms_avg": round(avg_ms, 4),
+            "kernel": "k_dsum128v64_lanes (phase A, lane per unit) + run scan (u64) + k_dec128v64w<2, Prefix>", "kernel_ms_avg": round(avg_ms, 4),
             "alg_bytes_per_launch": int(alg),
             "alg_bytes_def": "unit bytes + 2048 B decoded + 8 B offset per unit (phase A's read of the stream not counted)",
             "per_unit_starts_ms_avg": round(float(np.mean(plain_ms)), 4), "per_rank": per_rank}

@@ -52,7 +52,7 @@ KERNELS = {
     # D1 encode of the C3 posting list: plan + write passes (run scan not counted)
     "c3enc": ([_enc32("plan", True), _enc32("write", True)], "k_enc256v32_plan<true> + k_enc256v32_write<true>"),
     # 64-bit chained list: phase A (unit sums) + phase B (prefix decode)
-    "c3chain64": ([_dec64(2, 3), _dec64(2, 2)], "k_dec128v64w<2,Sum> (phase A) + k_dec128v64w<2,Prefix>"),
+    "c3chain64": ([lambda n: "k_dsum128v64_lanes" in n, _dec64(2, 2)], "k_dsum128v64_lanes (phase A) + k_dec128v64w<2,Prefix>"),
 }
 
 

@@ -77,17 +77,19 @@ def test_round3_kernels(tmp_path):
 
 def test_round4_kernels(tmp_path):
     """c3enc = the D1 encoder's two passes; c3chain64 = the 64-bit chained
-    decode's Sum and Prefix launches (mangled names, as rocprofv3 may print)."""
+    decode's lane-per-unit phase A and its Prefix launch (mangled names, as
+    rocprofv3 may print; the decoder's Sum and PerUnit modes are not counted)."""
     out = tmp_path / "t.json"
     pl1 = "_ZN3tpf3dev16k_enc256v32_planILb1ELi0EEEvPKjm"
     wr1 = "_ZN3tpf3dev17k_enc256v32_writeILb1ELi0EEEvPKjm"
     pl0 = "_ZN3tpf3dev16k_enc256v32_planILb0ELi0EEEvPKjm"
     d = _run(tmp_path, "c3enc", [(pl1, 3), (wr1, 4), (pl0, 99)], [(pl1, 0), (wr1, 7), (pl0, 99)], out)
     assert d["FETCH_SIZE_KiB_median"] == 7 and d["WRITE_SIZE_KiB_median"] == 7
+    la = "_ZN3tpf3dev18k_dsum128v64_lanesILj2ELj16384EEEvNS0_9Dec64ArgsE"
     s3 = "_ZN3tpf3dev12k_dec128v64wILj2ELNS0_7Start64E3EEEvNS0_9Dec64ArgsE"
     s2 = "_ZN3tpf3dev12k_dec128v64wILj2ELNS0_7Start64E2EEEvNS0_9Dec64ArgsE"
     s1 = "_ZN3tpf3dev12k_dec128v64wILj2ELNS0_7Start64E1EEEvNS0_9Dec64ArgsE"
-    d = _run(tmp_path, "c3chain64", [(s3, 10), (s2, 20), (s1, 500)], [(s3, 0), (s2, 40), (s1, 500)], out)
+    d = _run(tmp_path, "c3chain64", [(la, 10), (s2, 20), (s3, 77), (s1, 500)], [(la, 0), (s2, 40), (s3, 77), (s1, 500)], out)
     assert d["FETCH_SIZE_KiB_median"] == 30 and d["WRITE_SIZE_KiB_median"] == 40
 
 
