@@ -834,6 +834,10 @@ def run_c4(args, world, rank, dev, T):
     _, enc64_ms = T.run(enc_64, s64, 1)
     _, dec64_ms = T.run(lambda: tpf.dec_batch("256v64", enc64["p"], enc64["o"], nb, 256, out=out64), s64, 1)
     p64 = int(enc64["p"].numel())
+    # the 256v64 decoder's own data-movement probe on the same stream (its loads and stores, no decode)
+    probe64_ms = None
+    if hasattr(tpf.lib(), "tpf_probe256v64"):
+        _, probe64_ms = T.run(lambda: tpf.probe256v64(enc64["p"], enc64["o"], nb, out64), s64, 1)
     del v64, out64, enc64, bufs64
     torch.cuda.empty_cache()
 
@@ -860,6 +864,11 @@ def run_c4(args, world, rank, dev, T):
            "roundtrip_256v64": {"nblocks": nb, "G_int64_per_s": round(nb * 256 / (el64 / s64) / 1e9, 2),
                                 "enc_G_int64_per_s": g(nb, enc64_ms), "dec_G_int64_per_s": g(nb, dec64_ms),
                                 "packed_bytes_per_unit": round(p64 / nb, 1), "verified": ok64}}
+    if probe64_ms is not None:
+        cfg["roundtrip_256v64"].update({
+            "dec_alg_GBps": gbs(a64_dec, dec64_ms), "probe_GBps": gbs(a64_dec, probe64_ms),
+            "dec_ms_vs_probe": round(float(np.mean(dec64_ms)) / float(np.mean(probe64_ms)), 3),
+            "probe_def": "tpf_probe256v64 on the same stream (the decoder's loads + stores, no decode)"})
     # roofline of the step (encode = plan + offset scan + write launches, then
     # the decode launch, all on the launch stream): algorithmic bytes are the
     # encoder's (1024 in + block out + 8 offset) plus the decoder's (block in

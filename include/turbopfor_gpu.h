@@ -53,6 +53,12 @@ int tpf_p4dec256v32_batch(const uint8_t *d_in, uint64_t in_bytes, const uint64_t
 int tpf_probe256v32(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks,
                     uint32_t *d_out, void *stream);
 
+/* Measurement only: the same for the 256v64 decoder (nunits 256v64 units at
+ * d_off, each unit's first staged bytes written to both 1 KB halves of its
+ * 2 KB output). */
+int tpf_probe256v64(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nunits,
+                    uint64_t *d_out, void *stream);
+
 /* Measurement only (no reference counterpart): the device's own streaming
  * ceilings, timed by bench.py in the same process as the codec.  kind 0 =
  * read `bytes` of d_src (d_dst receives at most one 16-byte sink word), 1 =

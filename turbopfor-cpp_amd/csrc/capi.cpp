@@ -107,6 +107,17 @@ int tpf_probe256v32(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_
     return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_probe256v32");
 }
 
+int tpf_probe256v64(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nunits, uint64_t * d_out,
+                    void * stream)
+{
+    if (int rc = check_device())
+        return rc;
+    if (nunits && (!d_in || !d_off || !d_out))
+        return fail(TPF_EINVAL, "tpf_probe256v64: null pointer");
+    hipError_t e = tpf::launch_probe128v64(2u, d_in, in_bytes, d_off, nunits, d_out, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_probe256v64");
+}
+
 int tpf_probe_hbm(int kind, void * d_dst, const void * d_src, uint64_t bytes, void * stream)
 {
     if (int rc = check_device())

@@ -60,10 +60,12 @@ constexpr uint32_t kPos64 = TPF_D64_POS;
 
 // Decode one 128v64 block at LDS byte s into lane t's values 2t, 2t+1.
 // Returns the consumed bytes (wave-uniform).  scr: 2 * kPos64 u64 per wave.
+// hw: the block's first 4 bytes when the caller has them in registers
+// (wave-uniform), ~0u to read them from LDS.
 __device__ __forceinline__ uint32_t decode_block128v64(const uint32_t * lds, uint32_t s, uint64_t * scr, uint32_t t, uint64_t & x0,
-                                                       uint64_t & x1)
+                                                       uint64_t & x1, uint32_t hwin = ~0u)
 {
-    const uint32_t hw = uni(lds_u32(lds, s));
+    const uint32_t hw = hwin != ~0u ? hwin : uni(lds_u32(lds, s));
     const uint32_t h = hw & 0xFFu, x1b = (hw >> 8) & 0xFFu;
     if ((h & 0xC0u) == 0xC0u)
     {
@@ -137,12 +139,16 @@ __device__ __forceinline__ uint64_t delta1_128v64(uint64_t & x0, uint64_t & x1, 
 //           list decodes with only its initial start
 //   Sum     phase A of the chained decode: each unit's delta total
 //           sum(v + 1) mod 2^64 (decoded, not stored) and one total per run
+//   Probe   measurement only: the same loads and stores with the decoding
+//           removed (the 256v32 decoder's Probe mode), the data-movement
+//           ceiling of the pipeline on a given stream
 enum class Start64 : int
 {
     None = 0,
     PerUnit = 1,
     Prefix = 2,
     Sum = 3,
+    Probe = 4,
 };
 
 struct Dec64Args
@@ -174,6 +180,11 @@ template <uint32_t NB, Start64 SM>
 // Round-4 A/B on C4 (profiles/r4f_d64_time.log): ONE + 4 in flight + 6 waves
 // 457 G int64/s, ONE + 6 in flight 456, 4 in flight alone 448, the earlier
 // TWO + 3 + 4 waves 445.
+// first block's header from the load registers instead of LDS (A/B knob;
+// round 4, profiles/r4y_d64_ab.txt: level on C4, -0.5..-2% on C3 64-bit lists)
+#ifndef TPF_D64_HEAD
+#define TPF_D64_HEAD 0
+#endif
 #ifndef TPF_D64_NC
 #define TPF_D64_NC 4
 #endif
@@ -193,7 +204,7 @@ __global__ __launch_bounds__(256, TPF_D64_MINW) void k_dec128v64w(const Dec64Arg
     uint64_t * out = A.out;
     unsigned long long * err = A.err;
     __shared__ uint32_t slots[4][kSlot64 / 4];
-    __shared__ uint64_t scratch[4][2 * kPos64];
+    __shared__ __attribute__((aligned(16))) uint64_t scratch[4][2 * kPos64];
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
     uint32_t * slot = slots[wv];
@@ -227,6 +238,17 @@ __global__ __launch_bounds__(256, TPF_D64_MINW) void k_dec128v64w(const Dec64Arg
 #endif
 
     auto consume = [&](const Chunk & c, uint32_t jj) {
+        if constexpr (SM == Start64::Probe)
+        {
+            // the unit's loads (the rest of a unit over 1 KB too), NB 1 KB stores
+            typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+            const u32x4 a = c.a | (TPF_D64_ONE ? P.big_rest_or(jj, t) : c.b);
+            const u64x2 x{(static_cast<uint64_t>(a.y) << 32) | a.x, (static_cast<uint64_t>(a.w) << 32) | a.z};
+#pragma unroll
+            for (uint32_t u = 0; u < NB; ++u)
+                __builtin_nontemporal_store(x, reinterpret_cast<u64x2 *>(out_run + (jj * NB + u) * 128u) + t);
+            return;
+        }
         const uint32_t ctl = P.stage(c, jj, slot, t);
         uint32_t s = (ctl >> kCtlShift) & 15u;
         const uint32_t s0 = s;
@@ -237,7 +259,12 @@ __global__ __launch_bounds__(256, TPF_D64_MINW) void k_dec128v64w(const Dec64Arg
         for (uint32_t u = 0; u < NB; ++u)
         {
             uint64_t x0, x1;
+#if TPF_D64_HEAD
+            // the first block's header from the load registers (the 256v32 path's head())
+            const uint32_t used = decode_block128v64(slot, s, scr, t, x0, x1, u == 0 ? P.head(c, ctl, slot) : ~0u);
+#else
             const uint32_t used = decode_block128v64(slot, s, scr, t, x0, x1);
+#endif
             s += used & ~kWidthBad; // a flagged first block: the second is still parsed in the slot
             wbad |= used & kWidthBad;
             if constexpr (SM == Start64::Sum)
@@ -289,6 +316,8 @@ __global__ __launch_bounds__(256, TPF_D64_MINW) void k_dec128v64w(const Dec64Arg
         if (t == 0)
             A.run_tot[first / kRun] = rt;
     }
+    if constexpr (SM == Start64::Probe)
+        return;
     const uint64_t badmask = usedv.bad(P.len, valid);
     if (err != nullptr && t == 0 && badmask != 0u)
         atomicMin(err, static_cast<unsigned long long>(first + __builtin_ctzll(badmask)));
@@ -564,6 +593,16 @@ hipError_t launch_dec128v64(uint32_t nb, const uint8_t * in, uint64_t in_bytes, 
         return hipSuccess;
     dev::Dec64Args A{in, in_bytes, off, nunits, out, starts, 0ull, nullptr, nullptr, nullptr, nullptr, err};
     return starts ? launch64<dev::Start64::PerUnit>(nb, A, s) : launch64<dev::Start64::None>(nb, A, s);
+}
+
+// Measurement only: k_dec128v64w's loads and stores without the decoding.
+hipError_t launch_probe128v64(uint32_t nb, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nunits, uint64_t * out,
+                              hipStream_t s)
+{
+    if (nunits == 0)
+        return hipSuccess;
+    dev::Dec64Args A{in, in_bytes, off, nunits, out, nullptr, 0ull, nullptr, nullptr, nullptr, nullptr, nullptr};
+    return launch64<dev::Start64::Probe>(nb, A, s);
 }
 
 // Chained delta-1 decode of a 64-bit list (128v64 / 256v64 units chained the

@@ -76,6 +76,8 @@ hipError_t launch_d1chain_decode(const uint8_t * in, uint64_t in_bytes, const ui
 
 hipError_t launch_dec128v64(uint32_t nb, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nunits,
                             uint64_t * out, const uint64_t * starts, unsigned long long * err, hipStream_t s);
+hipError_t launch_probe128v64(uint32_t nb, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nunits, uint64_t * out,
+                              hipStream_t s);
 
 size_t d1chain64_workspace(uint64_t nunits);
 hipError_t launch_d1chain64_sums(uint32_t nb, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nunits, void * ws,

@@ -123,6 +123,9 @@ def lib():
             L.tpf_d1dec64_chain_decode.argtypes = [ctypes.c_int, c_vp, c_u64, c_vp, c_u64, c_vp, c_u64, c_vp, c_vp, c_vp]
             for name in ("tpf_d1dec64_chained", "tpf_d1dec64_chain_sums", "tpf_d1dec64_chain_decode"):
                 getattr(L, name).restype = ctypes.c_int
+        if hasattr(L, "tpf_probe256v64"):
+            L.tpf_probe256v64.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp]
+            L.tpf_probe256v64.restype = ctypes.c_int
         for name in ("tpf_p4nenc256v32", "tpf_p4ndec256v32", "tpf_p4dec256v32_batch", "tpf_p4d1dec256v32_batch", "tpf_p4enc256v32_batch",
                      "tpf_p4d1enc256v32_batch", "tpf_dec_batch", "tpf_enc_batch", "tpf_p4d1dec256v32_chained",
                      "tpf_p4d1dec256v32_chain_sums", "tpf_p4d1dec256v32_chain_decode", "tpf_probe256v32",
@@ -162,6 +165,15 @@ def dec256v32(packed, offsets, nblocks, out=None, starts=None, err=None):
         rc = L.tpf_p4d1dec256v32_batch(_ptr(packed), packed.numel(), _ptr(offsets), nblocks, _ptr(out),
                                        _ptr(starts), _ptr(err), _stream(torch))
     _check(rc)
+    return out
+
+
+def probe256v64(packed, offsets, nunits, out):
+    """Measurement only: the 256v64 decode kernel's loads and stores without
+    the decoding (tpf_probe256v64)."""
+    import torch
+
+    _check(lib().tpf_probe256v64(_ptr(packed), packed.numel(), _ptr(offsets), nunits, _ptr(out), _stream(torch)))
     return out
 
 
