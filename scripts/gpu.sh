@@ -7,7 +7,7 @@
 #   prof:WL          rocprofv3 --kernel-trace --stats of a bench -> ${TAG}_WL_prof/
 #   pmc:WL           FETCH_SIZE and WRITE_SIZE passes (separate runs) + pmc_traffic.py
 #                    -> gpurun_out/pmc_traffic.json (starts from profiles/pmc_traffic.json)
-#   ab:WL            LIBS="tree ablib/x.so" ROUNDS=2: bench per library build
+#   ab:WL            LIBS="tree ablib/x.so" ENVS="A=1 A=2" ROUNDS=2: bench per library build x env
 #   libs:SCRIPT[:ARGS] python SCRIPT once per library build in LIBS     -> ${TAG}_SCRIPT.log
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS (comma list)           -> ${TAG}_SCRIPT.log
 set -o pipefail
@@ -53,10 +53,12 @@ for f in glob.glob(sys.argv[1] + '/**/*kernel_stats.csv', recursive=True):
       wl=$rest
       for i in $(seq ${ROUNDS:-2}); do
         for lib in ${LIBS:-tree}; do
+         for ev in ${ENVS:-none}; do
           if [ $lib = tree ]; then unset TPF_LIB; else export TPF_LIB=$R/$lib; fi
-          n=$(basename $lib .so)
-          timeout -k 10 240 python bench.py --workload $wl --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --no-probes ${BARGS} > $O/${T}_ab_${wl}_${n}_$i.json 2> $O/${T}_ab_${wl}_${n}_$i.err || fail "ab $n" $? $O/${T}_ab_${wl}_${n}_$i.err 5
+          n=$(basename $lib .so); [ $ev = none ] || n=${n}_${ev//=/}
+          timeout -k 10 240 env ${ev/#none/TPF_AB=0} python bench.py --workload $wl --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --no-probes ${BARGS} > $O/${T}_ab_${wl}_${n}_$i.json 2> $O/${T}_ab_${wl}_${n}_$i.err || fail "ab $n" $? $O/${T}_ab_${wl}_${n}_$i.err 5
           python -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['config']; r=d['roofline']; print(sys.argv[3], sys.argv[2], d['value'], 'ms', r.get('kernel_ms_avg'), 'verified', c.get('verified'), {k: v for k, v in c.items() if k.endswith('per_s')})" $O/${T}_ab_${wl}_${n}_$i.json $n $wl
+         done
         done
       done ;;
     libs)

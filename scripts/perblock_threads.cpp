@@ -1,0 +1,100 @@
+// perblock_threads.cpp -- aggregate throughput of the per-block drop-in calls
+// (include/turbopfor.h: one 256-value block per call, any number of calling
+// threads, src/dispatch.cpp:88-104) at T concurrent callers: each thread
+// encodes / decodes ITS OWN block K times with turbopfor::p4Enc256v32 /
+// p4Dec256v32, checking every returned end pointer and the decoded values.
+// One JSON line per T.
+// usage: perblock_threads K T1 [T2 ...]
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "turbopfor.h"
+
+static void fill_block(uint32_t * v, uint32_t seed)
+{
+    // bw 8 base with 10% exceptions in [2^8, 2^32): the ab_test-style mix (ab_test.cpp:1611-1626)
+    uint64_t x = 0x9E3779B97F4A7C15ull * (seed + 1);
+    for (int i = 0; i < 256; ++i)
+    {
+        x ^= x << 13;
+        x ^= x >> 7;
+        x ^= x << 17;
+        v[i] = (x % 10 == 0) ? static_cast<uint32_t>(256u + (x >> 32) % 0xFFFFFEFFu) : static_cast<uint32_t>((x >> 20) & 255u);
+    }
+}
+
+int main(int argc, char ** argv)
+{
+    if (argc < 3)
+    {
+        std::fprintf(stderr, "usage: %s K T1 [T2 ...]\n", argv[0]);
+        return 2;
+    }
+    const int K = std::atoi(argv[1]);
+    for (int a = 2; a < argc; ++a)
+    {
+        const int T = std::atoi(argv[a]);
+        std::atomic<int> bad{0};
+        double dec_s = 0, enc_s = 0;
+        for (int phase = 0; phase < 2; ++phase) // 0 = encode, 1 = decode
+        {
+            std::atomic<int> ready{0};
+            std::atomic<bool> go{false};
+            std::vector<std::thread> th;
+            std::vector<double> secs(T);
+            for (int i = 0; i < T; ++i)
+                th.emplace_back([&, i] {
+                    uint32_t v[256], out[256];
+                    unsigned char buf[4096];
+                    fill_block(v, static_cast<uint32_t>(i));
+                    unsigned char * end = turbopfor::p4Enc256v32(v, 256, buf); // warm: also relaunches the server
+                    if (!end)
+                    {
+                        bad++;
+                        return;
+                    }
+                    ready++;
+                    while (!go.load())
+                        std::this_thread::yield();
+                    const auto t0 = std::chrono::steady_clock::now();
+                    for (int k = 0; k < K; ++k)
+                    {
+                        if (phase == 0)
+                        {
+                            if (turbopfor::p4Enc256v32(v, 256, buf) != end)
+                                bad++;
+                        }
+                        else if (turbopfor::p4Dec256v32(buf, 256, out) != end)
+                            bad++;
+                    }
+                    secs[i] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                    if (phase == 1 && std::memcmp(out, v, sizeof v) != 0)
+                        bad++;
+                });
+            while (ready.load() + bad.load() < T)
+                std::this_thread::yield();
+            const auto t0 = std::chrono::steady_clock::now();
+            go = true;
+            for (auto & t : th)
+                t.join();
+            const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            (phase == 0 ? enc_s : dec_s) = wall;
+        }
+        const double calls = static_cast<double>(T) * K;
+        std::printf("{\"threads\": %d, \"calls_per_thread\": %d, \"dec_calls_per_s\": %.0f, \"dec_G_int32_per_s\": %.4f, "
+                    "\"dec_us_per_call\": %.2f, \"enc_calls_per_s\": %.0f, \"enc_G_int32_per_s\": %.4f, \"enc_us_per_call\": %.2f, "
+                    "\"bad\": %d}\n",
+                    T, K, calls / dec_s, calls * 256 / dec_s / 1e9, dec_s * T / calls * 1e6, calls / enc_s, calls * 256 / enc_s / 1e9,
+                    enc_s * T / calls * 1e6, bad.load());
+        std::fflush(stdout);
+        if (bad.load())
+            return 1;
+    }
+    return 0;
+}

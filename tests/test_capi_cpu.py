@@ -106,3 +106,19 @@ def test_framing_matches_golden(lib, fname, fmt):
         assert lib.tpf_scan_offsets(FMT[fmt], stream, len(stream), n, len(encs), off) == len(stream)
         exp = np.concatenate([[0], np.cumsum([len(e) for e in encs])])
         assert list(off) == exp.tolist()
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/include/hip/hip_runtime.h"), reason="no HIP headers")
+def test_nested_perblock_pauses(lib, tmp_path):
+    """round 4's hs_pause A/B variant aborted with EDEADLK --
+    one thread locked the per-block pause (a std::shared_mutex) while holding
+    it.  tpf::PerblockPause now counts its own per-thread depth, so nested
+    pauses, tpf_perblock_quiesce and tpf_host_release inside a pause, on four
+    threads at once, neither throw nor hang (host only: no server runs)."""
+    exe = tmp_path / "pause_nesting"
+    subprocess.check_call(["g++", "-std=c++20", "-O1", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                           os.path.join(ROOT, "tests", "cpp", "pause_nesting.cpp"), "-L", os.path.dirname(LIB),
+                           "-lturbopfor_amd", "-Wl,-rpath," + os.path.dirname(LIB), "-lpthread", "-o", str(exe)])
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "pause nesting ok" in r.stdout

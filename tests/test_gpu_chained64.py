@@ -198,3 +198,45 @@ def test_chained64_repeated_positions():
     torch.cuda.synchronize()
     assert int(err.item()) == -1
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint64), exp)
+
+
+def test_dec64_position_past_block_flagged():
+    """A 128v64 vbyte block whose position byte points past its 128 values
+    (a corrupt stream: an encoder never writes one) is reported through d_err,
+    and the exception is dropped instead of being OR-ed into element pos-128
+    (ADVICE r4).  Units before it decode exactly, in the plain 256v64 decoder
+    and the chained 64-bit decode."""
+    fmt, nu, width, start0 = "256v64", 40, 256, 1 << 33
+    rng = np.random.default_rng(9)
+    gaps = rng.integers(0, 40, size=(nu, width)).astype(np.uint64)
+    exc = rng.random((nu, width)) < 0.05
+    gaps = np.where(exc, rng.integers(1 << 20, 1 << 30, size=(nu, width), dtype=np.uint64), gaps)
+    with np.errstate(over="ignore"):
+        vals = (np.cumsum(gaps.reshape(-1) + np.uint64(1), dtype=np.uint64) + np.uint64(start0)).reshape(nu, width)
+    starts = np.concatenate([np.array([start0], dtype=np.uint64), vals[:-1, -1]])
+    units = [bytearray(oracle_lib.encode(fmt, vals[i], d1=True, start=int(starts[i]))) for i in range(nu)]
+    bad_unit = None
+    for i in range(5, nu):
+        r = _vb64_positions(bytes(units[i]))
+        if r is not None and r[1] > r[0]:
+            units[i][r[0]] = 200
+            bad_unit = i
+            break
+    assert bad_unit is not None
+    packed_np = np.frombuffer(b"".join(bytes(u) for u in units), dtype=np.uint8)
+    offs_np = np.concatenate([[0], np.cumsum([len(u) for u in units])]).astype(np.int64)
+    packed = torch.from_numpy(packed_np.copy()).to(DEV)
+    offs = torch.from_numpy(offs_np).to(DEV)
+    st = _dev64(starts)
+    err = torch.zeros(1, dtype=torch.int64, device=DEV)
+    out = tpf.dec_batch(fmt, packed, offs, nu, width, starts=st, err=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == bad_unit
+    got = out.cpu().numpy().view(np.uint64).reshape(nu, width)
+    np.testing.assert_array_equal(got[:bad_unit], vals[:bad_unit])
+    err.zero_()
+    out = tpf.dec64_chained(fmt, packed, offs, nu, start0=start0, err=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == bad_unit
+    got = out.cpu().numpy().view(np.uint64).reshape(nu, width)
+    np.testing.assert_array_equal(got[:bad_unit], vals[:bad_unit])

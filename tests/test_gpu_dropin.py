@@ -288,10 +288,12 @@ def test_host_streams_of_two_threads_overlap():
     assert max(a0, b0) < min(a1, b1), f"calls ran one after the other: {spans}"
 
 
-def test_per_block_server_concurrent_threads():
-    """Eight threads share the block server's four mailboxes: every thread's
-    encode -> decode round trip of its own blocks is byte-exact (oracle) and
-    bit-exact."""
+@pytest.mark.parametrize("nthreads", [16, 80])
+def test_per_block_server_concurrent_threads(nthreads):
+    """16 threads (each its own mailbox) and 80 (more than the server's 64
+    mailboxes: callers wait for a free one) call at once: every thread's
+    encode -> decode round trip of its own blocks is byte-exact (oracle),
+    bit-exact, and every returned end pointer is right."""
     import threading
 
     L = capi()
@@ -305,7 +307,7 @@ def test_per_block_server_concurrent_threads():
 
     def worker(k):
         try:
-            blocks = datagen.c2_blocks(60, 3 + 3 * k, 10, seed=k)
+            blocks = datagen.c2_blocks(40 if nthreads <= 16 else 12, 1 + (3 * k) % 32, 10, seed=k)
             for v in blocks:
                 v = np.ascontiguousarray(v)
                 buf = np.zeros(4096, np.uint8)
@@ -319,7 +321,7 @@ def test_per_block_server_concurrent_threads():
         except Exception as e:  # noqa: BLE001
             errors.append((k, repr(e)))
 
-    ts = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(nthreads)]
     for t in ts:
         t.start()
     for t in ts:
@@ -506,17 +508,30 @@ def test_host_enc_multi_vs_single():
              ("256v32 D1 starts", 2, vals, 1, starts, 0, oracle_lib.enc256v32_batch(vals, starts=starts)),
              ("256v64 plain", 5, v64, 0, None, 0, oracle_lib.enc256v64_batch(v64)),
              ("2 blocks", 2, blocks[:2], 0, None, 0, oracle_lib.enc256v32_batch(blocks[:2]))]
+    L.tpf_enc_bound.restype = ctypes.c_uint64
+    L.tpf_enc_bound.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint]
     for k in (2, 3):
         devs = np.array([i % ndev for i in range(k)], dtype=np.int32)
         for name, fmt, v, d1, st, s0, (exp_p, exp_o) in cases:
             nb = len(v)
-            out = np.zeros(nb * 2200 + 64, dtype=np.uint8)
-            off = np.zeros(nb + 1, dtype=np.uint64)
-            rc = L.tpf_host_enc_multi(devs.ctypes.data, k, fmt, v.ctypes.data, nb, 256, d1,
-                                      None if st is None else st.ctypes.data, s0, out.ctypes.data, len(out), off.ctypes.data)
-            assert rc == 0, (name, k, L.tpf_last_error())
-            np.testing.assert_array_equal(off, exp_o, err_msg=f"{name} k={k}")
-            assert np.array_equal(out[: int(off[-1])], exp_p), (name, k)
+            # roomy output: shards written in place at provisional offsets and
+            # moved down; exactly the bound: shards through scratch buffers
+            for cap in (nb * 2200 + 64 * k + 64, int(L.tpf_enc_bound(fmt, nb, 256))):
+                out = np.zeros(cap, dtype=np.uint8)
+                off = np.zeros(nb + 1, dtype=np.uint64)
+                rc = L.tpf_host_enc_multi(devs.ctypes.data, k, fmt, v.ctypes.data, nb, 256, d1,
+                                          None if st is None else st.ctypes.data, s0, out.ctypes.data, len(out), off.ctypes.data)
+                assert rc == 0, (name, k, cap, L.tpf_last_error())
+                np.testing.assert_array_equal(off, exp_o, err_msg=f"{name} k={k} cap={cap}")
+                assert np.array_equal(out[: int(off[-1])], exp_p), (name, k, cap)
+    # bad (fmt, n) is rejected before any shard reads the caller's array
+    # (a chained shard read value n-1 of the unit before it first)
+    devs = np.zeros(2, dtype=np.int32)
+    out = np.zeros(len(vals) * 2200, dtype=np.uint8)
+    off = np.zeros(len(vals) + 1, dtype=np.uint64)
+    for fmt, n in ((2, 0), (2, 300), (2, 257), (5, 100), (99, 256)):
+        assert L.tpf_host_enc_multi(devs.ctypes.data, 2, fmt, vals.ctypes.data, len(vals), n, 1, None, 0,
+                                    out.ctypes.data, len(out), off.ctypes.data) == -1, (fmt, n)
     small = np.zeros(16, dtype=np.uint8)
     off = np.zeros(len(blocks) + 1, dtype=np.uint64)
     devs = np.zeros(2, dtype=np.int32)

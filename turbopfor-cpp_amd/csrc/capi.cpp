@@ -300,7 +300,7 @@ int tpf_probe_enc256v32(int mode, const uint32_t * d_in, uint64_t nblocks, uint8
 {
     if (int rc = check_device())
         return rc;
-    if (mode < 0 || mode > 3 || !d_off || (nblocks && (!d_in || !d_out || !d_ws)))
+    if (mode < 0 || mode > 4 || !d_off || (nblocks && (!d_in || !d_out || !d_ws)))
         return fail(TPF_EINVAL, "tpf_probe_enc256v32: bad mode or null pointer");
     if (ws_bytes < tpf::enc256v32_workspace(nblocks))
         return fail(TPF_EINVAL, "tpf_probe_enc256v32: workspace too small");
@@ -316,7 +316,12 @@ int tpf_p4d1enc256v32_batch(const uint32_t * d_in, uint64_t nblocks, const uint3
                             "tpf_p4d1enc256v32_batch");
 }
 
-static bool fmt_ok(int fmt, unsigned n)
+extern "C++" {
+namespace tpf
+{
+// (fmt, n) pairs the batch entry points accept (also checked by the host
+// streams before they cut a batch into shards)
+bool fmt_ok(int fmt, unsigned n)
 {
     switch (fmt)
     {
@@ -335,6 +340,9 @@ static bool fmt_ok(int fmt, unsigned n)
             return false;
     }
 }
+} // namespace tpf
+}
+using tpf::fmt_ok;
 
 static unsigned unit_values(int fmt, unsigned n)
 {

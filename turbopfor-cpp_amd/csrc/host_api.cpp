@@ -186,10 +186,16 @@ struct Server
     tpf::ServerReq * rq_host_d = nullptr;
     tpf::ServerAns * an = nullptr;   // answers: coherent pinned host memory (host view)
     tpf::ServerAns * an_d = nullptr; // the same memory, device view
+    tpf::ServerCtl * ctl = nullptr; // device memory shared by the launch's workgroups
     std::atomic<tpf::ServerReq *> launched_rq{nullptr};
-    std::mutex mu; // launches, event queries, mailbox leases
-    std::condition_variable cv;
-    uint32_t free_mask = (1u << tpf::kServerBoxes) - 1u;
+    std::mutex mu; // launches, event queries
+    // mailbox leases: a lock-free mask (64 mailboxes since round 5); callers
+    // wait on lease_cv only when every mailbox is taken
+    static_assert(tpf::kServerBoxes == 64, "one bit per mailbox");
+    std::atomic<uint64_t> free_mask{~0ull};
+    std::atomic<int> waiters{0};
+    std::mutex lease_mu;
+    std::condition_variable lease_cv;
     std::atomic<uint32_t> reqno[tpf::kServerBoxes] = {};
 
     static void * pinned(size_t bytes, void ** dev_view)
@@ -210,6 +216,9 @@ struct Server
         an_d = static_cast<tpf::ServerAns *>(dv);
         rq_host = static_cast<tpf::ServerReq *>(pinned(sizeof(tpf::ServerReq), &dv));
         rq_host_d = static_cast<tpf::ServerReq *>(dv);
+        void * c = nullptr;
+        hip_check(hipMalloc(&c, sizeof(tpf::ServerCtl)), "server control words");
+        ctl = static_cast<tpf::ServerCtl *>(c);
         // Mode 0 writes the request mailboxes in device memory from the CPU,
         // which needs the whole of VRAM mapped into the CPU's address space
         // (a large BAR).  Without one the device-memory half is never created
@@ -239,7 +248,7 @@ struct Server
     // caller holds mu, no launch running
     void launch(tpf::ServerReq * rq)
     {
-        hip_check(tpf::launch_block_server(rq == rq_host ? rq_host_d : rq, an_d, stream), "block server launch");
+        hip_check(tpf::launch_block_server(rq == rq_host ? rq_host_d : rq, an_d, ctl, stream), "block server launch");
         hip_check(hipEventRecord(done, stream), "block server event");
         launched = true;
         launched_rq.store(rq, std::memory_order_release);
@@ -285,21 +294,38 @@ struct Server
         std::atomic_thread_fence(std::memory_order_seq_cst);
     }
 
+    // A free mailbox, searched from a per-thread starting bit (threads
+    // spread over the mask instead of all racing for the lowest bit).
     int lease()
     {
-        std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return free_mask != 0u; });
-        const int i = __builtin_ctz(free_mask);
-        free_mask &= ~(1u << i);
-        return i;
+        thread_local const uint32_t hint = [] {
+            static std::atomic<uint32_t> next{0};
+            return next.fetch_add(1u) % tpf::kServerBoxes;
+        }();
+        for (;;)
+        {
+            uint64_t m = free_mask.load(std::memory_order_relaxed);
+            while (m != 0u)
+            {
+                const uint64_t rot = (m >> hint) | (hint ? m << (64u - hint) : 0u); // bit j = mailbox (hint + j) % 64
+                const int i = static_cast<int>((hint + static_cast<uint32_t>(__builtin_ctzll(rot))) % tpf::kServerBoxes);
+                if (free_mask.compare_exchange_weak(m, m & ~(1ull << i), std::memory_order_acq_rel))
+                    return i;
+            }
+            std::unique_lock<std::mutex> g(lease_mu);
+            waiters.fetch_add(1);
+            lease_cv.wait(g, [&] { return free_mask.load() != 0u; });
+            waiters.fetch_sub(1);
+        }
     }
     void release(int i)
     {
+        free_mask.fetch_or(1ull << i);
+        if (waiters.load() > 0)
         {
-            std::lock_guard<std::mutex> g(mu);
-            free_mask |= 1u << i;
+            std::lock_guard<std::mutex> g(lease_mu);
+            lease_cv.notify_one();
         }
-        cv.notify_one();
     }
 
     // Make sure a launch serves `rq`.  Fast path: the running launch raised
@@ -364,8 +390,13 @@ Server * g_srv[64] = {};
 std::shared_mutex g_pause;
 std::atomic<int> g_pause_waiting{0};
 
+// pauses this thread holds (tpf::PerblockPause nests; only depth 0 -> 1 locks)
+thread_local int t_pause_depth = 0;
+
 std::shared_lock<std::shared_mutex> perblock_enter()
 {
+    if (t_pause_depth > 0)
+        return std::shared_lock<std::shared_mutex>(); // this thread already excludes every other server user
     while (g_pause_waiting.load(std::memory_order_acquire) > 0)
         std::this_thread::yield();
     return std::shared_lock<std::shared_mutex>(g_pause);
@@ -540,10 +571,25 @@ void set_last_error(const std::string & msg);
 
 PerblockPause::PerblockPause()
 {
-    pause_lock();
+    if (t_pause_depth++ == 0)
+    {
+        try
+        {
+            pause_lock();
+        }
+        catch (...)
+        {
+            --t_pause_depth;
+            throw;
+        }
+    }
     stop_servers();
 }
-PerblockPause::~PerblockPause() { g_pause.unlock(); }
+PerblockPause::~PerblockPause()
+{
+    if (--t_pause_depth == 0)
+        g_pause.unlock();
+}
 } // namespace tpf
 
 namespace
@@ -672,9 +718,7 @@ extern "C" {
 
 void tpf_perblock_quiesce(void)
 {
-    pause_lock();
-    stop_servers();
-    g_pause.unlock();
+    const tpf::PerblockPause p; // nests inside a pause this thread already holds
 }
 
 int tpf_perblock_mode(int mode)

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <optional>
 #include <thread>
@@ -144,6 +145,19 @@ Reach reach(const void * ptr, size_t bytes)
         // reports the queried address, so that test sent every pinned torch
         // buffer through the pageable staging: host encode 12.9 -> 9.8 G
         // int32/s, decode 12.3 -> 10.9, round 4.)
+        // Both ends must lie in ONE allocation: the mapped device address r.d
+        // is derived from lo's, and the kernels' direct paths address the whole
+        // range through it.  A range across two registrations,
+        // or one HIP cannot size, is staged.
+        hipDeviceptr_t base = nullptr;
+        size_t size = 0;
+        if (hipMemGetAddressRange(&base, &size, const_cast<uint8_t *>(lo)) != hipSuccess || !base ||
+            hi >= static_cast<const uint8_t *>(base) + size || lo < static_cast<const uint8_t *>(base))
+        {
+            (void)hipGetLastError();
+            r.direct = false;
+            return r;
+        }
         if (a.devicePointer && a.hostPointer)
             r.d = static_cast<uint8_t *>(a.devicePointer) + (lo - static_cast<const uint8_t *>(a.hostPointer));
         return r;
@@ -185,20 +199,9 @@ void par_copy(void * dst, const void * src, size_t n)
 // the library's own buffers and streams (HIP waits for every stream of the
 // device there, the server's included), so those -- and only those -- hold
 // tpf::PerblockPause.  Host-stream calls of different threads otherwise run
-// concurrently (the whole call used to hold it).  Reentrant per thread.
-thread_local int t_pause_depth = 0;
-struct FreePause
-{
-    std::optional<tpf::PerblockPause> p;
-    FreePause()
-    {
-        if (t_pause_depth++ == 0)
-            p.emplace();
-    }
-    ~FreePause() { --t_pause_depth; }
-    FreePause(const FreePause &) = delete;
-    FreePause & operator=(const FreePause &) = delete;
-};
+// concurrently (the whole call used to hold it).  Reentrant per
+// thread (tpf::PerblockPause counts its own depth).
+using FreePause = tpf::PerblockPause;
 
 // A grow-only device (or pinned host) buffer.
 struct Buf
@@ -716,6 +719,13 @@ int tpf_host_enc_multi(const int * devs, int ndev, int fmt, const void * h_vals,
         h_off[0] = 0;
         if (nblocks == 0)
             return TPF_OK;
+        // validate before any shard reads the caller's array (a chained D1
+        // shard reads the value before its first block: with n == 0 or n past
+        // the unit that read would leave the array)
+        if (!tpf::fmt_ok(fmt, n))
+            throw Err(TPF_EINVAL, "tpf_host_enc_multi: unsupported (fmt, n)");
+        if (!h_vals || !h_out)
+            throw Err(TPF_EINVAL, "tpf_host_enc_multi: null pointer");
         need_device();
         int cnt = 0;
         hc(hipGetDeviceCount(&cnt), "hipGetDeviceCount");
@@ -730,8 +740,17 @@ int tpf_host_enc_multi(const int * devs, int ndev, int fmt, const void * h_vals,
         std::vector<uint64_t> cut(static_cast<size_t>(ndev) + 1);
         for (int d = 0; d <= ndev; ++d)
             cut[d] = nblocks * static_cast<uint64_t>(d) / static_cast<uint64_t>(ndev);
-        // shard d > 0: into its own host buffer (worst case of its blocks), offsets into h_off's slots
-        std::vector<std::vector<uint8_t>> tmp(static_cast<size_t>(ndev));
+        // Shard d > 0 writes at a provisional offset: the worst case of the
+        // shards before it, inside the caller's own output when out_cap holds
+        // every shard's bound (then each shard is moved down into place once
+        // the earlier sizes are known: final <= provisional), else into a
+        // scratch buffer of its bound (no zero-fill).  ADVICE r4: the first
+        // version always used zero-filled pageable vectors, copied twice.
+        std::vector<uint64_t> prov(static_cast<size_t>(ndev) + 1, 0);
+        for (int d = 0; d < ndev; ++d)
+            prov[d + 1] = prov[d] + tpf_enc_bound(fmt, cut[d + 1] - cut[d], n);
+        const bool in_place = prov[ndev] <= out_cap;
+        std::vector<std::unique_ptr<uint8_t[]>> tmp(static_cast<size_t>(ndev));
         std::vector<std::vector<uint64_t>> toff(static_cast<size_t>(ndev));
         std::vector<int> rc(static_cast<size_t>(ndev), TPF_OK);
         std::vector<std::string> msg(static_cast<size_t>(ndev));
@@ -760,9 +779,15 @@ int tpf_host_enc_multi(const int * devs, int ndev, int fmt, const void * h_vals,
                     rc[d] = tpf_host_enc(fmt, vals, nb, n, d1, st, s0, h_out, out_cap, h_off);
                 else
                 {
+                    const uint64_t cap = prov[d + 1] - prov[d];
+                    uint8_t * dst = h_out + prov[d];
                     try
                     {
-                        tmp[d].resize(tpf_enc_bound(fmt, nb, n));
+                        if (!in_place)
+                        {
+                            tmp[d].reset(new uint8_t[cap]);
+                            dst = tmp[d].get();
+                        }
                         toff[d].resize(nb + 1);
                     }
                     catch (const std::exception & e)
@@ -771,7 +796,7 @@ int tpf_host_enc_multi(const int * devs, int ndev, int fmt, const void * h_vals,
                         msg[d] = e.what();
                         return;
                     }
-                    rc[d] = tpf_host_enc(fmt, vals + b0 * uv * es, nb, n, d1, st, s0, tmp[d].data(), tmp[d].size(), toff[d].data());
+                    rc[d] = tpf_host_enc(fmt, vals + b0 * uv * es, nb, n, d1, st, s0, dst, cap, toff[d].data());
                 }
                 if (rc[d] != TPF_OK)
                     msg[d] = tpf_last_error(); // thread-local: carried to the caller's thread below
@@ -782,7 +807,8 @@ int tpf_host_enc_multi(const int * devs, int ndev, int fmt, const void * h_vals,
             if (rc[d] != TPF_OK)
                 throw Err(rc[d], "tpf_host_enc_multi: shard " + std::to_string(d) + " (device " + std::to_string(devs[d]) + ", blocks " +
                                      std::to_string(cut[d]) + ".." + std::to_string(cut[d + 1]) + "): " + msg[d]);
-        // move the later shards into place behind the earlier ones
+        // move the later shards into place behind the earlier ones, in order
+        // (each destination ends at or before its provisional source)
         for (int d = 1; d < ndev; ++d)
         {
             const uint64_t b0 = cut[d], nb = cut[d + 1] - cut[d];
@@ -791,7 +817,12 @@ int tpf_host_enc_multi(const int * devs, int ndev, int fmt, const void * h_vals,
             const uint64_t pos = h_off[b0], total = toff[d][nb];
             if (pos + total > out_cap)
                 throw Err(TPF_EINVAL, "tpf_host_enc_multi: out_cap too small");
-            par_copy(h_out + pos, tmp[d].data(), total);
+            const uint8_t * src = in_place ? h_out + prov[d] : tmp[d].get();
+            if (!in_place || pos + total <= prov[d])
+                par_copy(h_out + pos, src, total); // disjoint ranges
+            else if (pos != prov[d])
+                std::memmove(h_out + pos, src, total);
+            tmp[d].reset();
             for (uint64_t i = 1; i <= nb; ++i)
                 h_off[b0 + i] = pos + toff[d][i];
         }

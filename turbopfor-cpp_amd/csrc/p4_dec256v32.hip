@@ -62,7 +62,7 @@ struct DecArgs
 // Measured and kept: runs of 16 (8: same, 32..62:
 // -2..-5%), 7 waves/SIMD; ONE/NC=6 beat two loads/NC=3 by 1-2% (C2) and
 // 2-6% (C3); deeper pipelines lose occupancy.
-// GB != 0 (round 4, A/B knob TPF_DEC_GROUP): the pipeline moves GROUPS of
+// GB != 0 (round 4; chosen per launch since round 5, launch_mode): the pipeline moves GROUPS of
 // consecutive blocks whose bytes fit one GB-byte window from the first
 // block's 16-aligned start (one ballot per group: block ends ascend) instead
 // of single blocks, so a wave keeps ~NC KB of reads in flight whatever the
@@ -475,20 +475,29 @@ namespace
 #ifndef TPF_DEC_POL
 #define TPF_DEC_POL (2 | 8)
 #endif
-// grouped loads (A/B knob, 0 = one load per block): window bytes and run length
-#ifndef TPF_DEC_GROUP
-#define TPF_DEC_GROUP 0
-#endif
-#ifndef TPF_DEC_GROUP_RUN
-#define TPF_DEC_GROUP_RUN 32
-#endif
+// Grouped loads (round 5: chosen per launch).  A stream of
+// small blocks moves 1 KB GROUPS of consecutive blocks through the pipeline
+// (GB = 1024) instead of one block per load: round 4's A/B per bit width
+// (profiles/r4e_dec_groups.txt, 10M blocks each) had it 7% faster at 166-194
+// B per block (bw 1-2), 2% at 252 B (bw 4), level at 367 B (bw 8) and 3-4%
+// slower at 482-636 B (bw 12-17): two blocks sharing a window decode one after
+// the other inside one pipeline slot.  So a launch whose blocks average under
+// kGroupMeanBytes takes the grouped kernel, every other launch (C2's mix
+// averages 607 B) the single-block pipeline.  Both are exact on any stream: a
+// block larger than the window is a group of one.
+constexpr uint64_t kGroupMeanBytes = 300;
 template <dev::StartMode SM>
 hipError_t launch_mode(const dev::DecArgs & A, hipStream_t stream)
 {
-    constexpr uint32_t run = TPF_DEC_GROUP ? TPF_DEC_GROUP_RUN : dev::kRunDefault;
+    constexpr uint32_t run = dev::kRunDefault;
     constexpr uint64_t per_wg = 4ull * run;
     const uint32_t grid = static_cast<uint32_t>((A.nblocks + per_wg - 1) / per_wg);
-    hipLaunchKernelGGL((dev::k_dec256v32w<SM, run, TPF_DEC_POL, 6, 7, true, TPF_DEC_GROUP>), dim3(grid), dim3(256), 0, stream, A);
+    // (plain decode only: the delta-1 modes' grouped form spills at 7 waves/SIMD)
+    if ((SM == dev::StartMode::None || SM == dev::StartMode::Probe) && A.in_bytes < kGroupMeanBytes * A.nblocks)
+        hipLaunchKernelGGL((dev::k_dec256v32w<SM, run, TPF_DEC_POL, 6, 7, true, (SM == dev::StartMode::None || SM == dev::StartMode::Probe) ? 1024u : 0u>),
+                           dim3(grid), dim3(256), 0, stream, A);
+    else
+        hipLaunchKernelGGL((dev::k_dec256v32w<SM, run, TPF_DEC_POL, 6, 7, true, 0>), dim3(grid), dim3(256), 0, stream, A);
     return hipGetLastError();
 }
 } // namespace

@@ -13,7 +13,16 @@
 namespace tpf
 {
 
-size_t enc256v32_workspace(uint64_t nblocks) { return enc256::twopass_workspace(nblocks); }
+size_t enc256v32_workspace(uint64_t nblocks) { return enc256::slot_workspace(nblocks); }
+
+static int enc_path()
+{
+    static const int p = [] {
+        const char * e = getenv("TPF_ENC_PATH");
+        return e ? atoi(e) : 0;
+    }();
+    return p;
+}
 
 // probe (measurement / test hooks, reachable only through tpf_probe_enc256v32):
 //   0 / 3 production: the two-pass encoder
@@ -24,13 +33,20 @@ hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_
 {
     if (nblocks == 0)
         return fill_u32(off, 0u, 2, stream);
-    if (nblocks + 1 > 0x7FFFFFFFull || ws_bytes < enc256v32_workspace(nblocks))
+    if (nblocks + 1 > 0x7FFFFFFFull || ws_bytes < enc256::twopass_workspace(nblocks))
         return hipErrorInvalidValue;
+    const bool slot_ok = ws_bytes >= enc256::slot_workspace(nblocks);
     switch (probe)
     {
         case 0:
         case 3:
+            if (slot_ok && enc_path() == 2)
+                return enc256::launch_slot(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream);
             return enc256::launch_twopass<0, 0>(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream);
+        case 4:
+            if (!slot_ok)
+                return hipErrorInvalidValue;
+            return enc256::launch_slot(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream);
         case 1:
             return enc256::launch_twopass<1, 0>(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream);
         case 2:

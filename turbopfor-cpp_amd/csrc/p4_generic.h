@@ -143,8 +143,8 @@ __device__ __forceinline__ uint32_t vbyte_len(uint32_t m)
 // vbyte exceptions into scr[pos] (T per position, zeroed here).  Same
 // 64-byte window parse as vbyte_exceptions in p4_block32.h, generic width.
 // NPOS: scratch entries of scr and of tmp (256; 128 for the 128-value 64-bit
-// blocks, whose valid positions and exception counts are < 128: malformed
-// ones alias inside the scratch instead of leaving it)
+// blocks, whose valid positions and exception counts are < 128: a malformed
+// position past them is dropped and flagged with kWidthBad)
 // 64-bit vbyte scratch cleared by one 16-byte store per lane instead of two
 // 8-byte stores (A/B knob; round 4, profiles/r4y_d64_ab.txt: C3 64-bit lists
 // +2.5%, C4's 64-bit leg level)
@@ -175,6 +175,7 @@ __device__ __forceinline__ uint32_t vbyte_exceptions_g(const uint32_t * lds, uin
     wave_lds_sync();
     const uint32_t first = uni(lds_byte(lds, v0));
     uint32_t vend;
+    bool badpos = false;
     constexpr uint32_t ES = Wide ? 8u : 4u;
     if (first == 0xFFu)
     {
@@ -182,7 +183,10 @@ __device__ __forceinline__ uint32_t vbyte_exceptions_g(const uint32_t * lds, uin
         for (uint32_t k = t; k < xn; k += 64u)
         {
             const T val = Wide ? static_cast<T>(lds_u64(lds, v0 + 1u + ES * k)) : static_cast<T>(lds_u32(lds, v0 + 1u + ES * k));
-            atomicOr(&scr[lds_byte(lds, pbase + k) & PM], val);
+            const uint32_t pos = lds_byte(lds, pbase + k);
+            badpos |= pos > PM;
+            if (pos <= PM)
+                atomicOr(&scr[pos], val);
         }
         vend = pbase;
     }
@@ -209,10 +213,18 @@ __device__ __forceinline__ uint32_t vbyte_exceptions_g(const uint32_t * lds, uin
         }
         wave_lds_sync();
         for (uint32_t k = t; k < xn; k += 64u)
-            atomicOr(&scr[lds_byte(lds, vend + k) & PM], tmp[k & PM]);
+        {
+            const uint32_t pos = lds_byte(lds, vend + k);
+            badpos |= pos > PM;
+            if (pos <= PM)
+                atomicOr(&scr[pos], tmp[k & PM]);
+        }
     }
     wave_lds_sync();
-    return vend + xn;
+    // a position past the block (only possible with NPOS 128) is dropped, not
+    // aliased into a real element, and flags the block like a bad width
+    // (the reference writes it past the 128 values it unpacks)
+    return (vend + xn) | ((NPOS < 256u && __builtin_amdgcn_ballot_w64(badpos) != 0ull) ? kWidthBad : 0u);
 }
 
 // Decode one block of format F (n values) staged at LDS byte s.  v[j] gets

@@ -6,7 +6,8 @@
 // (src/dispatch.cpp:88-95 on one core).  Here one workgroup stays resident
 // while calls keep coming: wave w polls request box w (tpf_server.h: in
 // fine-grained device memory the host writes through the BAR, or in pinned
-// host memory), decodes or encodes the block it finds with the generic wave
+// host memory; 16 workgroups x 4 waves = 64 mailboxes since round 5), decodes
+// or encodes the block it finds with the generic wave
 // codec (p4_generic.h: every format of turbopfor.h; 256v64 = two 128v64
 // blocks, p4enc256v64_scalar.cpp:15-30), writes the result into answer box w
 // in pinned host memory and acknowledges.  Host and device exchange only
@@ -124,15 +125,23 @@ __device__ __forceinline__ void srv_serve(SrvLds & L, const ServerReqBox * box, 
         T last = T(0);
         uint32_t used = srv_dec_one<F>(L, 0u, n0, d1, static_cast<T>(start), out, t, &lim, &last);
         uint32_t written = lim;
-        if (pair && n > 128u && used < in_len)
+        // a pair whose first block consumes all of in_len disagrees with the
+        // host framing of both blocks: corrupt input, not a 128-value success
+        // 
+        bool ok = true;
+        if (pair && n > 128u)
         {
-            // second 128v64 block, starting after the first one's value 127
-            used += srv_dec_one<F>(L, used, n - 128u, d1, last, out + 128, t, &lim, &last);
-            written = 128u + lim;
+            ok = used < in_len;
+            if (ok)
+            {
+                // second 128v64 block, starting after the first one's value 127
+                used += srv_dec_one<F>(L, used, n - 128u, d1, last, out + 128, t, &lim, &last);
+                written = 128u + lim;
+            }
         }
         if (t == 0)
         {
-            ans->result = used == in_len ? used : 0xFFFFFFFFu;
+            ans->result = ok && used == in_len ? used : 0xFFFFFFFFu;
             ans->written = written;
         }
         return;
@@ -158,24 +167,28 @@ __device__ __forceinline__ void srv_serve(SrvLds & L, const ServerReqBox * box, 
         ans->result = size;
 }
 
-__global__ __launch_bounds__(256) void k_block_server(ServerReq * rq, ServerAns * an, uint64_t idle_ticks, uint64_t max_ticks)
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t * p)
 {
-    __shared__ SrvLds L[kServerBoxes];
-    __shared__ uint64_t last_active;
-    __shared__ uint32_t quit;
+    return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256) void k_block_server(ServerReq * rq, ServerAns * an, ServerCtl * ctl, uint64_t idle_ticks,
+                                                      uint64_t max_ticks)
+{
+    __shared__ SrvLds L[kServerWavesPerWG];
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t w = uni(threadIdx.x >> 6);
     const uint64_t born = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0)
     {
-        last_active = born;
-        quit = 0u;
-    }
-    if (threadIdx.x == 0)
+        atomicAdd(&ctl->live, 1u);
+        atomicMax(&ctl->last_active, static_cast<unsigned long long>(born));
         __hip_atomic_store(&an->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     __syncthreads();
-    const ServerReqBox * box = &rq->box[w];
-    ServerAnsBox * ans = &an->box[w];
+    const uint32_t bi = blockIdx.x * kServerWavesPerWG + w; // this wave's mailbox
+    const ServerReqBox * box = &rq->box[bi];
+    ServerAnsBox * ans = &an->box[bi];
     uint32_t last = uni(ld_sys(&ans->ack));
     const uint32_t * line = &box->req;
     for (uint32_t polls = 0;; ++polls)
@@ -225,31 +238,36 @@ __global__ __launch_bounds__(256) void k_block_server(ServerReq * rq, ServerAns 
                 __hip_atomic_store(&ans->ack, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             last = r;
             if (t == 0)
-                atomicMax(reinterpret_cast<unsigned long long *>(&last_active),
-                          static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+                atomicMax(&ctl->last_active, static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
             if (__builtin_amdgcn_s_memrealtime() - born > max_ticks) // busy past the lifetime: leave after this answer
             {
                 if (t == 0)
-                    quit = 1u;
+                    __hip_atomic_store(&ctl->quit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
             continue;
         }
-        // leave together: once one wave quits (idle or told to stop) the others follow
+        // leave together: once one wave of the launch quits (idle or told to
+        // stop) every other follows; the shared words are read every 16th poll
+        // (the stop word every 64th: each read of it crosses PCIe in mode 2)
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
-        // (the stop word is read every 64th poll: each read is a PCIe round trip)
-        if (uni(quit) != 0u || ((polls & 63u) == 0u && uni(ld_sys(&rq->stop)) != 0u) || now - last_active > idle_ticks ||
-            now - born > max_ticks)
+        if ((polls & 15u) == 0u)
         {
-            if (t == 0)
-                quit = 1u;
-            break;
+            const uint64_t la = __hip_atomic_load(&ctl->last_active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (uni(ld_agent(&ctl->quit)) != 0u || ((polls & 63u) == 0u && uni(ld_sys(&rq->stop)) != 0u) ||
+                now - uni64(la) > idle_ticks || now - born > max_ticks)
+            {
+                if (t == 0)
+                    __hip_atomic_store(&ctl->quit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
         }
         __builtin_amdgcn_s_sleep(1);
     }
-    // every wave has left its poll loop: no request is served after this point
+    // every wave of this workgroup has left its poll loop: none serves after
+    // this point; the launch's last workgroup out lowers `alive`
     __syncthreads();
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0 && atomicSub(&ctl->live, 1u) == 1u)
         __hip_atomic_store(&an->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -258,9 +276,14 @@ __global__ __launch_bounds__(256) void k_block_server(ServerReq * rq, ServerAns 
 namespace tpf
 {
 
-hipError_t launch_block_server(ServerReq * d_req, ServerAns * d_ans, hipStream_t s)
+hipError_t launch_block_server(ServerReq * d_req, ServerAns * d_ans, ServerCtl * d_ctl, hipStream_t s)
 {
-    hipLaunchKernelGGL(dev::k_block_server, dim3(1), dim3(256), 0, s, d_req, d_ans, kServerIdleTicks, kServerMaxTicks);
+    // the control words start at zero for every launch (a kernel, not a
+    // memset: DESIGN.md 8)
+    hipError_t e = fill_u32(d_ctl, 0u, sizeof(ServerCtl) / 4u, s);
+    if (e != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(dev::k_block_server, dim3(kServerWGs), dim3(256), 0, s, d_req, d_ans, d_ctl, kServerIdleTicks, kServerMaxTicks);
     return hipGetLastError();
 }
 

@@ -13,6 +13,10 @@ namespace tpf
 // stopped -- no per-block call starts -- while alive: wrap every hipFree /
 // hipHostFree / hipHostUnregister of the library's own buffers in one, since
 // HIP waits for all of the device's streams there, the server's included.
+// Reentrant per thread (a thread-local depth: only the outermost pause takes
+// the lock), and a per-block call made by a thread that holds a pause does not
+// take the shared side (a std::shared_mutex locked again by its holder throws
+// EDEADLK; round 4's hs_pause variant hit exactly that).
 struct PerblockPause
 {
     PerblockPause();
@@ -49,9 +53,13 @@ hipError_t fill_u32(void * p, uint32_t v, uint32_t n, hipStream_t s);
 // Per-block block server (p4_server.hip, tpf_server.h).
 struct ServerReq;
 struct ServerAns;
-hipError_t launch_block_server(ServerReq * d_req, ServerAns * d_ans, hipStream_t s);
+struct ServerCtl;
+hipError_t launch_block_server(ServerReq * d_req, ServerAns * d_ans, ServerCtl * d_ctl, hipStream_t s);
 // Measurement only: streaming read / write / copy ceilings (hbm_probe.hip).
 hipError_t launch_probe_hbm(int kind, void * dst, const void * src, uint64_t bytes, hipStream_t s);
+
+// (fmt, n) accepted by the batch entry points (capi.cpp)
+bool fmt_ok(int fmt, unsigned n);
 
 size_t generic_workspace(uint64_t nblocks);
 hipError_t launch_dec_generic(int fmt, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t n,

@@ -17,10 +17,10 @@
 //   device: sees req != last, acquire, serves, release, ack = r
 //   host  : sees ack == r, acquire, reads the result
 // The kernel raises ServerAns::alive while it runs (the host posts without
-// querying the launch's event) and exits once every mailbox has been idle for
-// kServerIdleTicks of the 100 MHz real-time clock (or at once when told to
-// stop); the host sees alive drop / the launch complete and relaunches it on
-// the next request.
+// querying the launch's event) and exits once every mailbox of the launch has
+// been idle for kServerIdleTicks of the 100 MHz real-time clock (or at once
+// when told to stop); the host sees alive drop / the launch complete and
+// relaunches it on the next request.
 #pragma once
 
 #include <stdint.h>
@@ -28,7 +28,14 @@
 namespace tpf
 {
 
-constexpr uint32_t kServerBoxes = 4;           // one wave per mailbox, one workgroup
+// One wave per mailbox, four per workgroup.  Round 5: sixteen workgroups
+// (64 mailboxes: 64 threads call concurrently) instead of one (4 mailboxes:
+// a fifth calling thread waited for a free one).  The launch's
+// workgroups share one device-side control word set (ServerCtl) so they leave
+// together.
+constexpr uint32_t kServerWavesPerWG = 4;
+constexpr uint32_t kServerWGs = 16;
+constexpr uint32_t kServerBoxes = kServerWavesPerWG * kServerWGs;
 constexpr uint32_t kServerPayload = 8192;      // bytes in / out per request
 constexpr uint64_t kServerIdleTicks = 1000000; // 10 ms of s_memrealtime (100 MHz)
 // A launch also leaves after serving for 5 ms, busy or not (the next call
@@ -76,6 +83,15 @@ struct alignas(128) ServerReq
     uint32_t stop; // host -> device: exit now
     uint32_t pad[31];
     ServerReqBox box[kServerBoxes];
+};
+
+// Device memory (coarse-grained, zeroed before every launch): what the
+// launch's workgroups share.
+struct alignas(128) ServerCtl
+{
+    unsigned long long last_active; // s_memrealtime of the latest request served (or workgroup start)
+    uint32_t quit;                  // one workgroup decided to leave: the others follow
+    uint32_t live;                  // workgroups still serving; the last to leave lowers ServerAns::alive
 };
 
 struct alignas(128) ServerAns
