@@ -173,7 +173,7 @@ def traffic_fields(workload, nblocks):
 
 def hbm_probes(dev, nbytes=4 << 30):
     """The box's own streaming ceilings, measured in this run with the
-    library's probe kernels (tpf_probe_hbm: 16-B non-temporal read / write /
+    library's probe kernels (tpfm_probe_hbm: 16-B non-temporal read / write /
     copy, grid-stride): bytes moved (read + written) per second."""
     a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
@@ -192,7 +192,7 @@ def hbm_probes(dev, nbytes=4 << 30):
         torch.cuda.synchronize()
         res[kind + "_GBps"] = round(moved * 5 / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
     del a, b
-    res["def"] = ("tpf_probe_hbm over 4 GiB: read-only / write-only / copy (copy counts read + written bytes), "
+    res["def"] = ("tpfm_probe_hbm over 4 GiB: read-only / write-only / copy (copy counts read + written bytes), "
                   "16-B lanes, non-temporal, 128 WG/CU")
     return res
 
@@ -558,7 +558,7 @@ def run_c2(args, world, rank, dev, T, c5=False):
             "alg_bytes_per_launch": int(alg),
             "alg_bytes_def": "packed block bytes + 1024 B decoded + 8 B offset per block",
             "probe_GBps": round(probe, 1), "frac_of_probe": round(achieved / probe, 4),
-            "probe_def": "tpf_probe256v32: the decode kernel's own loads and stores with decoding removed",
+            "probe_def": "tpfm_probe256v32: the decode kernel's own loads and stores with decoding removed",
             "hbm_probes": probes, "per_rank": per_rank}
     # the CPU baseline is timed at N=1 only (a reported baseline, not a per-rank cost)
     cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(packed.cpu().numpy(),
@@ -765,7 +765,7 @@ def run_c3(args, world, rank, dev, T, chained):
                        else "tpf::dev::k_dec256v32w<StartMode::PerBlock>"),
             "probe_GBps": round(probe_alg / (float(np.mean(probe_ms)) * 1e-3) / 1e9, 1),
             "ms_vs_probe": round(avg_ms / float(np.mean(probe_ms)), 3),
-            "probe_def": "tpf_probe256v32 on the same stream (loads + stores, no decode; no starts read)",
+            "probe_def": "tpfm_probe256v32 on the same stream (loads + stores, no decode; no starts read)",
             "per_rank": per_rank}
     cfg = {"workload": "C3: p4D1Dec256v32 " + ("chained list (start0 only)" if chained else "per-block starts")
                        + ", Zipf(1.1) gaps on [1,64] + 5% 64+U[0,2^16)",
@@ -836,7 +836,7 @@ def run_c4(args, world, rank, dev, T):
     p64 = int(enc64["p"].numel())
     # the 256v64 decoder's own data-movement probe on the same stream (its loads and stores, no decode)
     probe64_ms = None
-    if hasattr(tpf.lib(), "tpf_probe256v64"):
+    if os.path.exists(tpf.MEASURE_PATH):
         _, probe64_ms = T.run(lambda: tpf.probe256v64(enc64["p"], enc64["o"], nb, out64), s64, 1)
     del v64, out64, enc64, bufs64
     torch.cuda.empty_cache()
@@ -868,7 +868,7 @@ def run_c4(args, world, rank, dev, T):
         cfg["roundtrip_256v64"].update({
             "dec_alg_GBps": gbs(a64_dec, dec64_ms), "probe_GBps": gbs(a64_dec, probe64_ms),
             "dec_ms_vs_probe": round(float(np.mean(dec64_ms)) / float(np.mean(probe64_ms)), 3),
-            "probe_def": "tpf_probe256v64 on the same stream (the decoder's loads + stores, no decode)"})
+            "probe_def": "tpfm_probe256v64 on the same stream (the decoder's loads + stores, no decode)"})
     # roofline of the step (encode = plan + offset scan + write launches, then
     # the decode launch, all on the launch stream): algorithmic bytes are the
     # encoder's (1024 in + block out + 8 offset) plus the decoder's (block in

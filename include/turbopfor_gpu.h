@@ -46,32 +46,6 @@ int tpf_device_count(void);
 int tpf_p4dec256v32_batch(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks,
                           uint32_t *d_out, uint64_t *d_err, void *stream);
 
-/* Measurement only (no reference counterpart): the decode kernel's exact load
- * and store pattern with the decoding removed -- block i's staged bytes are
- * written to d_out[256*i..] unchanged.  Gives the data-movement ceiling the
- * decoder is compared against in bench.py. */
-int tpf_probe256v32(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks,
-                    uint32_t *d_out, void *stream);
-
-/* Measurement only: the same for the 256v64 decoder (nunits 256v64 units at
- * d_off, each unit's first staged bytes written to both 1 KB halves of its
- * 2 KB output). */
-int tpf_probe256v64(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nunits,
-                    uint64_t *d_out, void *stream);
-
-/* Measurement only (no reference counterpart): the device's own streaming
- * ceilings, timed by bench.py in the same process as the codec.  kind 0 =
- * read `bytes` of d_src (d_dst receives at most one 16-byte sink word), 1 =
- * write `bytes` to d_dst, 2 = copy `bytes` from d_src to d_dst; 16-byte
- * lanes, non-temporal, grid-stride.  bytes is rounded down to 16. */
-int tpf_probe_hbm(int kind, void *d_dst, const void *d_src, uint64_t bytes, void *stream);
-/* Test hook (no product use): the run scan every two-pass kernel pair uses
- * between its passes (p4_scan.h).  d_tot: nruns u32 totals; writes
- * d_base[r] = sum of d_tot[0..r) (u64, exclusive) and *d_total = the sum of
- * all.  d_ws: tpf_test_run_scan_workspace_size(nruns) bytes. */
-size_t tpf_test_run_scan_workspace_size(uint64_t nruns);
-int tpf_test_run_scan(const uint32_t *d_tot, uint64_t nruns, uint64_t *d_base, uint64_t *d_total, void *d_ws, size_t ws_bytes,
-                      void *stream);
 
 /* Replaces turbopfor::p4D1Dec256v32 (include/turbopfor.h:42, dispatch.cpp:97-104):
  * block i is decoded with start d_starts[i] (the value preceding the block). */
@@ -141,15 +115,6 @@ int tpf_p4enc256v32_batch(const uint32_t *d_in, uint64_t nblocks, uint8_t *d_out
                           void *d_ws, size_t ws_bytes, void *stream);
 int tpf_p4d1enc256v32_batch(const uint32_t *d_in, uint64_t nblocks, const uint32_t *d_starts, uint32_t start0,
                             uint8_t *d_out, uint64_t out_cap, uint64_t *d_off, void *d_ws, size_t ws_bytes, void *stream);
-/* Measurement / test hooks (no reference counterpart): mode 1 = the two-pass
- * encoder's plan pass reduced to a wave OR, 2 = its write pass copying the
- * staged values (same loads and stores, output NOT a valid stream); 0 / 3 =
- * the two-pass encoder (plan, run scan, write; = tpf_p4enc256v32_batch).
- * Other modes: TPF_EINVAL.  (The rejected single-pass encoders of DESIGN.md
- * 4.4 are not in the library: scripts/enc_variants.hip.)  Arguments as
- * tpf_p4enc256v32_batch. */
-int tpf_probe_enc256v32(int mode, const uint32_t *d_in, uint64_t nblocks, uint8_t *d_out, uint64_t out_cap,
-                        uint64_t *d_off, void *d_ws, size_t ws_bytes, void *stream);
 
 /* ---- every format of include/turbopfor.h, batched ----------------------
  * fmt selects the reference function family:

@@ -1,7 +1,7 @@
 """Encoder kernel timing (measurement tool; run under rocprofv3 --kernel-trace
 --stats for per-kernel times): C4-mix 256v32 encode, `reps` launches.
 usage: python scripts/enc_kernel_times.py [nblocks] [reps] [probe]
-probe 1/2: tpf_probe_enc256v32 (the plan / write pass with the coding removed)"""
+probe 1/2: tpfm_enc256v32 modes 1/2 (the plan / write pass with the coding removed), 3 two-pass, 4 slot"""
 import os
 import sys
 
@@ -22,7 +22,7 @@ cap = int(tpf.lib().tpf_p4enc256v32_bound(nb))
 out = torch.empty(cap, dtype=torch.uint8, device=dev)
 for _ in range(reps):
     if probe:
-        tpf.probe_enc256v32(probe, vals, out)
+        tpf.enc256v32_path(probe, vals, out)
     else:
         tpf.enc256v32(vals, out=out)
 torch.cuda.synchronize()

@@ -143,3 +143,36 @@ def test_corrupt_offsets_reported():
     tpf.dec256v32(packed, torch.from_numpy(bad).to(DEV), len(blocks), err=err)
     torch.cuda.synchronize()
     assert int(err.item()) == 122
+
+
+@pytest.mark.parametrize("pad", [0, 5, 11])
+@pytest.mark.parametrize("mix", ["bw1-4", "bw1-4+wide"])
+def test_small_block_grouped_path_vs_oracle(pad, mix):
+    """Streams averaging under 300 B per block take the grouped-load kernel
+    (p4_dec256v32.h dec_grouped, round 5): consecutive blocks that fit one 1
+    KB window are staged and decoded together.  Bit-exact vs the oracle at
+    odd stream alignments, with blocks larger than a window mixed in (each a
+    group of one), and a corrupted offset still reported at its block."""
+    rng = np.random.default_rng(pad)
+    blocks = np.concatenate([datagen.c2_blocks(400, bw, exc, seed=pad + bw) for bw in (1, 2, 3, 4) for exc in (0, 10)])
+    if mix.endswith("wide"):
+        # a few bw-32 blocks (1025 B) and vbyte-heavy 24-bit blocks at random places
+        wide = np.concatenate([datagen.c2_blocks(6, 32, 0, seed=pad), datagen.c2_blocks(6, 24, 25, seed=pad + 1)])
+        at = np.sort(rng.choice(len(blocks), len(wide), replace=False))
+        blocks = np.insert(blocks, at, wide, axis=0)
+    packed_np, off_np = oracle_lib.enc256v32_batch(blocks)
+    assert len(packed_np) < 300 * len(blocks)
+    expect = oracle_lib.dec256v32_batch(packed_np, off_np, len(blocks))
+    packed, offs = to_dev_stream([packed_np.tobytes()], pad_front=pad)
+    err = torch.zeros(1, dtype=torch.int64, device=DEV)
+    out = tpf.dec256v32(packed, offs, len(blocks), err=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) & U64MAX == U64MAX
+    assert_blocks_equal(as_u32(out), expect, "grouped decode")
+    bad = off_np.astype(np.int64).copy()
+    bad[777] += 1
+    err.zero_()
+    out = tpf.dec256v32(packed, torch.from_numpy(bad).to(DEV), len(blocks), err=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 776
+    assert_blocks_equal(as_u32(out)[:776 * 256], expect[:776], "grouped decode before the corruption")

@@ -188,21 +188,16 @@ def test_run_scan_matches_cumsum(nruns):
     u64 prefix of u32 run totals near 2^32 (carries), across tile borders
     and across the single-workgroup top scan's 1024-tile steps (> 4M runs:
     sizes the encoders only reach at > 67M blocks)."""
-    L = tpf.lib()
-    L.tpf_test_run_scan_workspace_size.restype = ctypes.c_size_t
-    L.tpf_test_run_scan_workspace_size.argtypes = [ctypes.c_uint64]
-    L.tpf_test_run_scan.restype = ctypes.c_int
-    L.tpf_test_run_scan.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                    ctypes.c_size_t, ctypes.c_void_p]
+    M = tpf.measure()  # the test hook lives in the measurement library
     rng = np.random.default_rng(nruns)
     tot = rng.integers(0xF0000000, 1 << 32, nruns, dtype=np.uint64).astype(np.uint32)
     d_tot = torch.from_numpy(tot.view(np.int32)).to(DEV)
     d_base = torch.zeros(max(nruns, 1), dtype=torch.int64, device=DEV)
     d_total = torch.full((1,), -1, dtype=torch.int64, device=DEV)
-    wsb = int(L.tpf_test_run_scan_workspace_size(nruns))
+    wsb = int(M.tpfm_run_scan_workspace_size(nruns))
     ws = torch.empty(wsb, dtype=torch.uint8, device=DEV)
-    rc = L.tpf_test_run_scan(d_tot.data_ptr(), nruns, d_base.data_ptr(), d_total.data_ptr(), ws.data_ptr(), wsb,
-                             torch.cuda.current_stream().cuda_stream)
+    rc = M.tpfm_run_scan(d_tot.data_ptr(), nruns, d_base.data_ptr(), d_total.data_ptr(), ws.data_ptr(), wsb,
+                         torch.cuda.current_stream().cuda_stream)
     assert rc == 0
     torch.cuda.synchronize()
     incl = np.cumsum(tot.astype(np.uint64), dtype=np.uint64)

@@ -157,14 +157,15 @@ def test_full_size_c3_sample_vs_oracle():
     assert torch.equal(out2, vals)
 
 
-@pytest.mark.parametrize("mode", [0, 3])
-@pytest.mark.parametrize("nb", [1, 31, 33, 1000, 20_000])
+@pytest.mark.parametrize("mode", [0, 3, 4])
+@pytest.mark.parametrize("nb", [1, 15, 16, 17, 31, 33, 1000, 20_000])
 def test_encoder_entries_vs_oracle(mode, nb):
-    """The production 256v32 encoder through both entry points: 0 = the batch
-    entry (tpf_p4enc256v32_batch), 3 = the two-pass encoder through the probe
-    entry (tpf_probe_enc256v32).  Byte-exact vs the oracle, mixed widths and
-    exception rates, ragged last runs.  (The rejected single-pass encoders
-    live in scripts/enc_variants.hip: tests/test_gpu_enc_variants.py.)"""
+    """The 256v32 encoder through the batch entry (mode 0, the library's own
+    choice of path) and both paths forced through the measurement library
+    (tpfm_enc256v32): 3 = two-pass (plan, run scan, write), 4 = slot (plan +
+    build into per-run slots, run scan, compaction).  Byte-exact vs the
+    oracle, mixed widths and exception rates, ragged last runs (a run is 16
+    blocks)."""
     blocks = mixed_blocks(nb, nb + mode)
     exp_packed, exp_off = oracle_lib.enc256v32_batch(blocks)
     vals = dev_u32(blocks)
@@ -174,10 +175,30 @@ def test_encoder_entries_vs_oracle(mode, nb):
     else:
         cap = int(tpf.lib().tpf_p4enc256v32_bound(nb))
         out = torch.zeros(cap, dtype=torch.uint8, device=DEV)
-        offs = tpf.probe_enc256v32(mode, vals, out)
+        offs = tpf.enc256v32_path(mode, vals, out)
         packed = out.cpu().numpy()[:int(offs[-1].item())]
     np.testing.assert_array_equal(offs.cpu().numpy().astype(np.uint64), exp_off)
     np.testing.assert_array_equal(packed, exp_packed)
+
+
+@pytest.mark.parametrize("mode", [3, 4])
+@pytest.mark.parametrize("chained", [True, False])
+def test_encoder_paths_d1_vs_oracle(mode, chained):
+    """p4D1Enc256v32 through both forced paths, one chained C3 list (start0 +
+    the list itself) and per-block starts: byte-exact vs the oracle, and the
+    compaction's writes leave the bytes past the stream untouched."""
+    pv, st = datagen.c3_postings(3001)
+    exp_packed, exp_off = oracle_lib.enc256v32_batch(pv, starts=st)
+    vals = dev_u32(pv)
+    cap = int(tpf.lib().tpf_p4enc256v32_bound(len(pv)))
+    out = torch.full((cap,), 0xA5, dtype=torch.uint8, device=DEV)
+    starts = None if chained else dev_u32(st)
+    offs = tpf.enc256v32_path(mode, vals, out, d1=True, starts=starts, start0=int(st[0]))
+    got = out.cpu().numpy()
+    total = int(offs[-1].item())
+    np.testing.assert_array_equal(offs.cpu().numpy().astype(np.uint64), exp_off)
+    np.testing.assert_array_equal(got[:total], exp_packed)
+    assert (got[total:total + 4096] == 0xA5).all()
 
 
 def mixed_blocks(nb, seed):

@@ -96,50 +96,6 @@ int tpf_p4dec256v32_batch(const uint8_t * d_in, uint64_t in_bytes, const uint64_
     return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_p4dec256v32_batch");
 }
 
-int tpf_probe256v32(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nblocks, uint32_t * d_out,
-                    void * stream)
-{
-    if (int rc = check_device())
-        return rc;
-    if (nblocks && (!d_in || !d_off || !d_out))
-        return fail(TPF_EINVAL, "tpf_probe256v32: null pointer");
-    hipError_t e = tpf::launch_probe256v32(d_in, in_bytes, d_off, nblocks, d_out, static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_probe256v32");
-}
-
-int tpf_probe256v64(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nunits, uint64_t * d_out,
-                    void * stream)
-{
-    if (int rc = check_device())
-        return rc;
-    if (nunits && (!d_in || !d_off || !d_out))
-        return fail(TPF_EINVAL, "tpf_probe256v64: null pointer");
-    hipError_t e = tpf::launch_probe128v64(2u, d_in, in_bytes, d_off, nunits, d_out, static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_probe256v64");
-}
-
-int tpf_probe_hbm(int kind, void * d_dst, const void * d_src, uint64_t bytes, void * stream)
-{
-    if (int rc = check_device())
-        return rc;
-    if (kind < 0 || kind > 2 || !d_dst || (kind != 1 && !d_src))
-        return fail(TPF_EINVAL, "tpf_probe_hbm: bad kind or null pointer");
-    hipError_t e = tpf::launch_probe_hbm(kind, d_dst, d_src, bytes, static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_probe_hbm");
-}
-
-size_t tpf_test_run_scan_workspace_size(uint64_t nruns) { return tpf::test_run_scan_workspace(nruns); }
-
-int tpf_test_run_scan(const uint32_t * d_tot, uint64_t nruns, uint64_t * d_base, uint64_t * d_total, void * d_ws, size_t ws_bytes,
-                      void * stream)
-{
-    if (int rc = check_device())
-        return rc;
-    if (!d_total || (nruns && (!d_tot || !d_base || !d_ws)))
-        return fail(TPF_EINVAL, "tpf_test_run_scan: null pointer");
-    hipError_t e = tpf::test_run_scan(d_tot, nruns, d_base, d_total, d_ws, ws_bytes, static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_test_run_scan");
-}
 
 int tpf_p4d1dec256v32_batch(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nblocks, uint32_t * d_out,
                             const uint32_t * d_starts, uint64_t * d_err, void * stream)
@@ -295,19 +251,6 @@ int tpf_p4enc256v32_batch(const uint32_t * d_in, uint64_t nblocks, uint8_t * d_o
     return enc256v32_common(d_in, nblocks, nullptr, 0, false, d_out, out_cap, d_off, d_ws, ws_bytes, stream, "tpf_p4enc256v32_batch");
 }
 
-int tpf_probe_enc256v32(int mode, const uint32_t * d_in, uint64_t nblocks, uint8_t * d_out, uint64_t out_cap, uint64_t * d_off,
-                        void * d_ws, size_t ws_bytes, void * stream)
-{
-    if (int rc = check_device())
-        return rc;
-    if (mode < 0 || mode > 4 || !d_off || (nblocks && (!d_in || !d_out || !d_ws)))
-        return fail(TPF_EINVAL, "tpf_probe_enc256v32: bad mode or null pointer");
-    if (ws_bytes < tpf::enc256v32_workspace(nblocks))
-        return fail(TPF_EINVAL, "tpf_probe_enc256v32: workspace too small");
-    hipError_t e = tpf::launch_enc256v32(d_in, nblocks, nullptr, 0, false, d_out, out_cap, d_off, d_ws, ws_bytes,
-                                         static_cast<hipStream_t>(stream), mode);
-    return e == hipSuccess ? TPF_OK : hip_fail(e, "tpf_probe_enc256v32");
-}
 
 int tpf_p4d1enc256v32_batch(const uint32_t * d_in, uint64_t nblocks, const uint32_t * d_starts, uint32_t start0, uint8_t * d_out,
                             uint64_t out_cap, uint64_t * d_off, void * d_ws, size_t ws_bytes, void * stream)

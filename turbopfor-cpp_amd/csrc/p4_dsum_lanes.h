@@ -38,10 +38,7 @@
 namespace tpf::dev
 {
 
-#ifndef TPF_DSUM_RUN
-#define TPF_DSUM_RUN 64
-#endif
-constexpr uint32_t kLaneRun = TPF_DSUM_RUN; // blocks per wave run: lane j = block first + j (16 | kLaneRun <= 64)
+constexpr uint32_t kLaneRun = 64; // blocks per wave run: lane j = block first + j (16 | kLaneRun <= 64)
 
 // Per-width row of the SWAR digit-sum table (b = 0..32, 16 dwords each):
 // [0,5) keep masks A_l, [5,10) add masks B_l, [10,15) shifts w_l = b << l,
@@ -189,8 +186,8 @@ __device__ __forceinline__ uint32_t base_sum_lanes(const uint32_t * w, uint32_t 
     return bs;
 }
 
-#ifndef TPF_DSUM_SKIP
-#define TPF_DSUM_SKIP 0 // measurement builds only: 1 base payload, 2 compressed vbyte, 4 raw vbyte, 8 positions
+#ifndef TPF_DSUM_ABLATE
+#define TPF_DSUM_ABLATE 0 // measurement builds only (p4_dec256v32.hip): 1 base payload, 2 compressed vbyte, 4 raw vbyte, 8 positions
 #endif
 template <uint32_t LIM>
 __device__ __forceinline__ bool dsum_lanes(const uint32_t * w, uint32_t p, uint32_t len, bool act, const uint32_t * tab, uint32_t & sum)
@@ -247,7 +244,7 @@ __device__ __forceinline__ bool dsum_lanes(const uint32_t * w, uint32_t p, uint3
     const bool raw = is_vb && wbyte<LIM>(w, v0) == 0xFFu;
     const bool comp = is_vb && !raw;
     uint32_t vend = v0 + 1u + 4u * xn;
-    if ((TPF_DSUM_SKIP & 4) == 0 && __ballot(ok && raw) != 0ull)
+    if ((TPF_DSUM_ABLATE & 4) == 0 && __ballot(ok && raw) != 0ull)
     {
         // 8 values per step from 9 aligned dwords: one LDS round trip per step
         ok = ok && (!raw || vend + xn - p == len);
@@ -267,7 +264,7 @@ __device__ __forceinline__ bool dsum_lanes(const uint32_t * w, uint32_t p, uint3
                 exsum += on && k0 + u < xn ? __builtin_amdgcn_alignbyte(d[u + 1], d[u], m) : 0u;
         }
     }
-    if ((TPF_DSUM_SKIP & 2) == 0 && __ballot(ok && comp) != 0ull)
+    if ((TPF_DSUM_ABLATE & 2) == 0 && __ballot(ok && comp) != 0ull)
     {
         // Fast path, no serial marker chain: when every value is 1 or 2 bytes
         // (markers < 0xDC; C3's compressed blocks are all of this kind) the
@@ -373,7 +370,7 @@ __device__ __forceinline__ bool dsum_lanes(const uint32_t * w, uint32_t p, uint3
     // reference ORs exceptions that share a position (patch loop
     // p4d1dec256v32_scalar.cpp:260); the wave decoder takes those blocks.
     // 16 positions per step from 5 aligned dwords.
-    if ((TPF_DSUM_SKIP & 8) == 0 && __ballot(ok && is_vb) != 0ull)
+    if ((TPF_DSUM_ABLATE & 8) == 0 && __ballot(ok && is_vb) != 0ull)
     {
         const bool on = ok && is_vb;
         const uint32_t kmax = uni(wave_max_u32(on ? xn : 0u));
@@ -415,7 +412,7 @@ __device__ __forceinline__ bool dsum_lanes(const uint32_t * w, uint32_t p, uint3
     const uint32_t lmax = uni(wave_max_u32(on ? sum_levels(tab, b) : 0u));
     const uint32_t pmax = uni(wave_max_u32(on ? sum_pre(tab, b) : 0u));
     uint32_t bs = 0u;
-    if ((TPF_DSUM_SKIP & 1) == 0 && bmax != 0u)
+    if ((TPF_DSUM_ABLATE & 1) == 0 && bmax != 0u)
     {
         const uint32_t * row = tab + (on ? b : 0u) * kSumTabRow;
         const uint32_t key = pmax * 8u + lmax;

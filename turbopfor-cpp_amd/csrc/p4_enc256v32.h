@@ -2,8 +2,7 @@
 // p4D1Enc256v32, reference src/scalar/p4enc256v32_scalar.cpp:216-235 and
 // p4d1enc256v32_scalar.cpp:7-15) on gfx950: device code and its launch
 // sequence, shared by the library (p4_enc256v32.hip) and the measurement
-// tool scripts/enc_variants.hip (the rejected single-pass encoders, kept out
-// of the library and A/B-timed against this one).
+// library (measure/tpf_measure.hip: the pass probes and forced paths).
 //
 // Four launches:
 //   1. plan  : one wave per block evaluates p4Bits32 (parallel cost model,
@@ -22,12 +21,11 @@
 // the next two blocks in flight (the first version loaded one block per loop
 // iteration and waited for it: 5.0 and 5.4 ms per 10M blocks, latency-bound).
 //
-// PROBE (measurement only, reachable through tpf_probe_enc256v32 -- the
+// PROBE (measurement only, instantiated by measure/tpf_measure.hip -- the
 // output is NOT a valid stream): 1 = plan kernel with the cost model replaced
 // by a wave OR, 2 = write kernel copying the staged values instead of
 // building blocks; same loads and stores, so they time each pass's
-// data-movement ceiling (scripts/gpu_enc_probe.sh, profiles/r1_v4_enc_probe.txt).
-// Bits 8 / 9 select nt / sc1 value loads (A/B knobs of scripts/enc_variants.hip).
+// data-movement ceiling (profiles/archive/r1/r1_v4_enc_probe.txt).
 #pragma once
 
 #include "p4_scan.h"
@@ -40,19 +38,11 @@ namespace tpf::dev
 
 constexpr uint32_t kImgU32 = 592; // bytes per wave image: 4..7 lead + block (<= 2276 B) + slack, 16-B multiple
 constexpr uint32_t kEncRun = 16;  // blocks per wave run
-#ifndef TPF_ENC_NC_PLAN
-#define TPF_ENC_NC_PLAN 3
-#endif
-#ifndef TPF_ENC_NC_WRITE
-#define TPF_ENC_NC_WRITE 3
-#endif
-// cache policy of the plan pass's value loads (A/B knob: 2 = nt)
-#ifndef TPF_ENC_PLAN_AUX
-#define TPF_ENC_PLAN_AUX 0
-#endif
-// value chunks in flight per wave (NC: blocks j+1 .. j+NC-1 while j is encoded)
-constexpr uint32_t kEncNCPlan = TPF_ENC_NC_PLAN;
-constexpr uint32_t kEncNCWrite = TPF_ENC_NC_WRITE;
+// value chunks in flight per wave (NC: blocks j+1 .. j+NC-1 while j is
+// encoded).  Measured and not kept: 2 / 4 / 6 in flight, nt or
+// sc1 value loads, nt interior stores, dword copy-out.
+constexpr uint32_t kEncNCPlan = 3;
+constexpr uint32_t kEncNCWrite = 3;
 
 // deltaEnc1 (p4_scalar_internal.h:711-719): d[i] = in[i] - in[i-1] - 1, in[-1] = start.
 __device__ __forceinline__ u32x4 delta_encode(const u32x4 & v, uint32_t start, uint32_t t)
@@ -107,11 +97,9 @@ struct EncRun
         return true;
     }
 
-    // AUX: cache policy bits of the value loads (2 = nt, 16 = sc1; A/B knob)
-    template <int AUX = 0>
     __device__ __forceinline__ u32x4 load(uint32_t jj, uint32_t t) const
     {
-        return __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(jj * 1024u + 16u * t), 0, AUX);
+        return __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(jj * 1024u + 16u * t), 0, 0);
     }
 
     // Start value of block first+t for delta-1 (lanes t < n): the given
@@ -128,13 +116,13 @@ struct EncRun
     }
 
     // Pipelined walk: body(v, jj) for jj = 0..n-1 with NC blocks in flight.
-    template <uint32_t NC, int AUX = 0, class Body>
+    template <uint32_t NC, class Body>
     __device__ __forceinline__ void walk(uint32_t t, Body && body) const
     {
         u32x4 C[NC];
 #pragma unroll
         for (uint32_t u = 0; u + 1 < NC; ++u)
-            C[u] = load<AUX>(u, t);
+            C[u] = load(u, t);
         bool more = true;
         for (uint32_t j = 0; more; j += NC)
         {
@@ -143,7 +131,7 @@ struct EncRun
             {
                 if (more)
                 {
-                    C[(u + NC - 1) % NC] = load<AUX>(j + u + NC - 1, t);
+                    C[(u + NC - 1) % NC] = load(j + u + NC - 1, t);
                     body(C[u], j + u);
                     more = j + u + 1 < n;
                 }
@@ -151,10 +139,6 @@ struct EncRun
         }
     }
 };
-
-// PROBE of the two-pass kernels: bits 0-1 = probe kind (1 plan as a wave OR,
-// 2 write as a copy), bit 8 = nt value loads, bit 9 = sc1 value loads (A/B)
-constexpr int enc_load_aux(int probe) { return ((probe & 256) ? 2 : 0) | ((probe & 512) ? 16 : 0); }
 
 __device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t lane)
 {
@@ -169,11 +153,11 @@ __device__ __forceinline__ void plan_run(const EncRun & R, const uint32_t * in, 
     const uint32_t stv = D1 ? R.start_lane(in, starts, start0, t) : 0u;
     szv = 0u;
     pwv = 0u;
-    R.template walk<kEncNCPlan, enc_load_aux(PROBE) | TPF_ENC_PLAN_AUX>(t, [&](u32x4 v, uint32_t jj) {
+    R.template walk<kEncNCPlan>(t, [&](u32x4 v, uint32_t jj) {
         if constexpr (D1)
             v = delta_encode(v, rl32(stv, jj), t);
         Plan32 P;
-        if constexpr ((PROBE & 3) == 1)
+        if constexpr (PROBE == 1)
         {
             P.b = bw32(uni(wave_or(v.x | v.y | v.z | v.w)));
             P.bx = 0;
@@ -188,20 +172,6 @@ __device__ __forceinline__ void plan_run(const EncRun & R, const uint32_t * in, 
     });
 }
 
-// copy-out of a built block (A/B knob): 0 = 16-byte chunks with byte-store
-// edges (copy_out_image16), 1 = dword stores (copy_out_dw)
-#ifndef TPF_ENC_COPY_DW
-#define TPF_ENC_COPY_DW 0
-#endif
-__device__ __forceinline__ void copy_out(const uint32_t * img, uint32_t sb, uint64_t dst, uint32_t size, uint64_t cap_end, uint32_t t)
-{
-#if TPF_ENC_COPY_DW
-    copy_out_dw(img, sb, dst, size, cap_end, t);
-#else
-    copy_out_image16(img, sb, dst, size, cap_end, t);
-#endif
-}
-
 // Write a run: lane j of (szv, pwv, olo/ohi) = size, plan word and byte
 // offset of block R.first+j.  img: the wave's zeroed LDS image (left zeroed).
 template <bool D1, int PROBE = 0>
@@ -210,17 +180,17 @@ __device__ __forceinline__ void write_run(const EncRun & R, const uint32_t * in,
                                           uint32_t * val, uint64_t out_base, uint64_t cap_end, uint32_t t)
 {
     const uint32_t stv = D1 ? R.start_lane(in, starts, start0, t) : 0u;
-    R.template walk<kEncNCWrite, enc_load_aux(PROBE)>(t, [&](u32x4 v, uint32_t jj) {
+    R.template walk<kEncNCWrite>(t, [&](u32x4 v, uint32_t jj) {
         if constexpr (D1)
             v = delta_encode(v, rl32(stv, jj), t);
         const uint32_t size = rl32(szv, jj);
         const Plan32 P = unplan(rl32(pwv, jj), size);
         const uint64_t dst = out_base + ((static_cast<uint64_t>(rl32(ohi, jj)) << 32) | rl32(olo, jj));
-        if constexpr ((PROBE & 3) == 2)
+        if constexpr (PROBE == 2)
         {
             reinterpret_cast<u32x4 *>(img)[4 + t] = v;
             wave_lds_sync();
-            copy_out(img, kImgLead, dst, size, cap_end, t);
+            copy_out_image16(img, kImgLead, dst, size, cap_end, t);
             wave_lds_sync();
             zero_image(img, kImgU32 / 4u, t);
             wave_lds_sync();
@@ -228,7 +198,7 @@ __device__ __forceinline__ void write_run(const EncRun & R, const uint32_t * in,
         }
         const uint32_t sb = emit_block256<true>(img, val, P, v, t);
         wave_lds_sync();
-        copy_out(img, sb, dst, size, cap_end, t);
+        copy_out_image16(img, sb, dst, size, cap_end, t);
         wave_lds_sync();
         // only [0, sb + size) can be non-zero: clear it for the next block
         zero_image(img, min((sb + size + 15u) >> 4, kImgU32 / 4u), t);
@@ -240,25 +210,14 @@ __device__ __forceinline__ void write_run(const EncRun & R, const uint32_t * in,
 // The plan pass leaves each block's size in off[block] and one total per
 // wave run; p4_scan.h scans only the run totals; the write pass rebuilds the
 // offsets of its run from the run base and its sizes and writes them back.
-// gate (optional): the kernels run only if *gate != 0 -- the fallback of the
-// rejected look-back encoder (scripts/enc_variants.hip), enqueued behind it
-// and left at once unless that launch aborted; the library passes nullptr.
-// Workgroups walk their runs grid-stride, so gated launches can use a small
-// grid.
-__device__ __forceinline__ bool gated_off(const uint32_t * gate)
-{
-    return gate != nullptr && __hip_atomic_load(const_cast<uint32_t *>(gate), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
-}
 
 template <bool D1, int PROBE = 0>
 __global__ __launch_bounds__(256) void k_enc256v32_plan(const uint32_t * __restrict in, uint64_t nblocks,
                                                          const uint32_t * __restrict starts, uint32_t start0,
                                                          uint64_t * __restrict sizes, uint32_t * __restrict plan,
-                                                         uint32_t * __restrict run_tot, const uint32_t * gate)
+                                                         uint32_t * __restrict run_tot)
 {
     __shared__ __attribute__((aligned(16))) uint32_t hist[4][kPlanHistU32];
-    if (gated_off(gate))
-        return;
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
     for (uint64_t g = blockIdx.x;; g += gridDim.x)
@@ -282,12 +241,10 @@ __global__ __launch_bounds__(256) void k_enc256v32_write(const uint32_t * __rest
                                                           const uint32_t * __restrict starts, uint32_t start0,
                                                           uint64_t * __restrict off, const uint32_t * __restrict plan,
                                                           const uint64_t * __restrict run_pre, const uint64_t * __restrict run_tile,
-                                                          uint8_t * __restrict out, uint64_t out_cap, const uint32_t * gate)
+                                                          uint8_t * __restrict out, uint64_t out_cap)
 {
     __shared__ __attribute__((aligned(16))) uint32_t img_all[4][kImgU32];
     __shared__ __attribute__((aligned(16))) uint32_t val_all[4][kEncValU32];
-    if (gated_off(gate))
-        return;
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
     uint32_t * img = img_all[wv];
@@ -467,42 +424,40 @@ inline hipError_t launch_slot(const uint32_t * in, uint64_t nblocks, const uint3
 }
 
 // plan -> run scan -> write.  PP / PW: PROBE of the plan / write kernel (0 =
-// production).  gate != nullptr: the kernels run only if *gate != 0, on a
-// grid-stride grid of per_cu workgroups per CU (scripts/enc_variants.hip).
+// production; the probes are instantiated only by the measurement library,
+// measure/tpf_measure.hip).
 template <int PP, int PW>
 hipError_t launch_twopass(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, bool d1, uint8_t * out,
-                          uint64_t out_cap, uint64_t * off, void * ws, hipStream_t stream, const uint32_t * gate = nullptr,
-                          uint32_t per_cu = 8)
+                          uint64_t out_cap, uint64_t * off, void * ws, hipStream_t stream)
 {
     uint32_t * plan = static_cast<uint32_t *>(ws);
     const uint64_t nruns = enc_runs(nblocks);
     const RunScanWs<uint64_t> rs = RunScanWs<uint64_t>::carve(static_cast<uint8_t *>(ws) + al256(nblocks * 4u), nruns);
     const uint64_t per_wg = 4ull * dev::kEncRun;
-    const uint64_t full = (nblocks + per_wg - 1) / per_wg;
-    const uint32_t grid = static_cast<uint32_t>(gate ? std::min<uint64_t>(full, grid_cap(stream, per_cu)) : full);
+    const uint32_t grid = static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg);
     if constexpr (PP != 0 || PW != 0)
     {
         if (d1)
             return hipErrorInvalidValue; // the probes measure the plain encoder only
     }
     if (d1)
-        hipLaunchKernelGGL((dev::k_enc256v32_plan<true, 0>), dim3(grid), dim3(256), 0, stream, in, nblocks,
-                           starts, start0, off, plan, rs.tot, gate);
+        hipLaunchKernelGGL((dev::k_enc256v32_plan<true, 0>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
+                           rs.tot);
     else
         hipLaunchKernelGGL((dev::k_enc256v32_plan<false, PP>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
-                           rs.tot, gate);
+                           rs.tot);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return e;
-    e = launch_run_scan_u64(rs.tot, nruns, rs.pre, rs.tile, off + nblocks, stream, gate);
+    e = launch_run_scan_u64(rs.tot, nruns, rs.pre, rs.tile, off + nblocks, stream);
     if (e != hipSuccess)
         return e;
     if (d1)
         hipLaunchKernelGGL((dev::k_enc256v32_write<true, 0>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
-                           rs.pre, rs.tile, out, out_cap, gate);
+                           rs.pre, rs.tile, out, out_cap);
     else
         hipLaunchKernelGGL((dev::k_enc256v32_write<false, PW>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,
-                           rs.pre, rs.tile, out, out_cap, gate);
+                           rs.pre, rs.tile, out, out_cap);
     return hipGetLastError();
 }
 

@@ -3,11 +3,12 @@
 // p4d1enc256v32_scalar.cpp:7-15) on gfx950: the two-pass encoder of
 // p4_enc256v32.h (plan -> run scan -> write).
 //
-// Only production kernels and the two pass probes live in the library.  The
-// single-pass designs measured against this encoder and rejected in round 2
-// (decoupled look-back over LDS-held tiles, the MALL-chunked pipelined
-// launch, the persistent-grid form, load cache policies) are
-// in scripts/enc_variants.hip, built into scripts/libencvar.so for A/B runs.
+// Only production kernels live in the library (the pass probes are in the
+// measurement library, measure/tpf_measure.hip).  The single-pass designs
+// measured against the two-pass encoder and rejected in round 2 (decoupled
+// look-back over LDS-held tiles, the MALL-chunked pipelined launch, the
+// persistent-grid form) were A/B'd from scripts/enc_variants.hip
+// until round 4 (git history).
 #include "p4_enc256v32.h"
 
 namespace tpf
@@ -24,36 +25,20 @@ static int enc_path()
     return p;
 }
 
-// probe (measurement / test hooks, reachable only through tpf_probe_enc256v32):
-//   0 / 3 production: the two-pass encoder
-//   1 / 2 its plan / write pass with the coding removed (not a valid stream)
+// The path (round 5): the slot encoder (values read once,
+// p4_enc256v32.h) when the workspace holds the slots, else the two-pass
+// encoder.  TPF_ENC_PATH=1 / 2 forces two-pass / slot (A/B runs).
 hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, bool d1,
-                            uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t stream,
-                            int probe)
+                            uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t stream)
 {
     if (nblocks == 0)
         return fill_u32(off, 0u, 2, stream);
     if (nblocks + 1 > 0x7FFFFFFFull || ws_bytes < enc256::twopass_workspace(nblocks))
         return hipErrorInvalidValue;
     const bool slot_ok = ws_bytes >= enc256::slot_workspace(nblocks);
-    switch (probe)
-    {
-        case 0:
-        case 3:
-            if (slot_ok && enc_path() == 2)
-                return enc256::launch_slot(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream);
-            return enc256::launch_twopass<0, 0>(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream);
-        case 4:
-            if (!slot_ok)
-                return hipErrorInvalidValue;
-            return enc256::launch_slot(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream);
-        case 1:
-            return enc256::launch_twopass<1, 0>(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream);
-        case 2:
-            return enc256::launch_twopass<0, 2>(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream);
-        default:
-            return hipErrorInvalidValue;
-    }
+    if (slot_ok && enc_path() == 2)
+        return enc256::launch_slot(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream);
+    return enc256::launch_twopass<0, 0>(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream);
 }
 
 } // namespace tpf

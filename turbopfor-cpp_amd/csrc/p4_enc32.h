@@ -40,17 +40,6 @@ __device__ __forceinline__ uint32_t vblen32(uint32_t x)
     return 1u + (x >= 156u) + (x >= 16540u) + (x >= 2113692u) + (x > 0xFFFFFFu);
 }
 
-#ifndef TPF_PLAN_FFBH
-#define TPF_PLAN_FFBH 1
-#endif
-// shifted suffix sums of the cost model through the histogram's LDS (one
-// write, two ds_read2) instead of four bpermutes: the plan pass waits on its
-// LDS pipe, and this drops one LDS instruction per block -- plan 1.982 ->
-// 1.836 ms per 10M C4 blocks, encode 467-471 -> 479-483 G int32/s (A/B on one
-// box, profiles/r3_enc_suffix_lds_ab.txt)
-#ifndef TPF_PLAN_SUFFIX_LDS
-#define TPF_PLAN_SUFFIX_LDS 1
-#endif
 // v_ffbh_u32(x) + 1: 0 for x == 0 (ffbh returns -1), else clz(x) + 1 = 33 - bw32(x)
 __device__ __forceinline__ uint32_t ffbh1(uint32_t x)
 {
@@ -92,7 +81,6 @@ __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist
     }
     PlanHist::zero(hist, t);
     wave_lds_sync();
-#if TPF_PLAN_FFBH
     // bins keyed by v_ffbh_u32(x) + 1: 0 for x == 0, else 33 - bw32(x) -- two
     // VALU per value (ffbh, shift-add) instead of clz + zero select + address
     PlanHist::add(hist, ffbh1(v.x), t);
@@ -101,40 +89,18 @@ __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist
     PlanHist::add(hist, ffbh1(v.w), t);
     wave_lds_sync();
     const uint32_t cnt = PlanHist::get(hist, t == 0u ? 0u : (t <= 32u ? 33u - t : 64u)); // lane c: cnt[c] (0 for c > 32)
-#else
-    PlanHist::add(hist, bw32(v.x), t);
-    PlanHist::add(hist, bw32(v.y), t);
-    PlanHist::add(hist, bw32(v.z), t);
-    PlanHist::add(hist, bw32(v.w), t);
     wave_lds_sync();
-    const uint32_t cnt = PlanHist::get(hist, t); // lane c holds cnt[c] (0 for c > 32)
-#endif
-    wave_lds_sync();
-#if TPF_PLAN_SUFFIX_LDS
     // suffix sums S(k) = #values with bw > k, then
     // vbsum(b) = S(b) + S(b+7) + 2 S(b+15) + 3 S(b+19) + 4 S(b+25): the shifted
     // sums come back through the histogram's LDS (one write, two ds_read2)
-    // instead of four bpermutes of cnt
+    // instead of four bpermutes of cnt (the plan pass waits on its LDS pipe:
+    // plan 1.982 -> 1.836 ms per 10M C4 blocks, round 3)
     const uint32_t incl = wave_incl_scan(cnt);
     const uint32_t ec = __builtin_amdgcn_readlane(incl, 63) - incl; // sum_{c > t} cnt[c]
     hist[t] = ec;                                                    // lanes >= 32 hold 0
     wave_lds_sync();
     const uint32_t vbsum = ec + hist[t + 7u] + 2u * hist[t + 15u] + 3u * hist[t + 19u] + 4u * hist[t + 25u]; // lanes t > 38: unused
     wave_lds_sync();
-#else
-    auto at = [&](uint32_t c) -> uint32_t {
-        // ds_bpermute takes lane c mod 64 from address bits [7:2]
-        const uint32_t x = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(c << 2), static_cast<int>(cnt)));
-        return c < 64u ? x : 0u;
-    };
-    const uint32_t vbacc = at(t + 7u) + 2u * at(t + 15u) + 3u * at(t + 19u) + 4u * at(t + 25u);
-    // both suffix sums in ONE scan: cnt <= 256 in the low half, cnt + vbacc
-    // <= 5*256 in the high half (no carry between the halves)
-    const uint32_t pab = wave_incl_scan(cnt | ((cnt + vbacc) << 16));
-    const uint32_t tab = __builtin_amdgcn_readlane(pab, 63);
-    const uint32_t ec = (tab & 0xFFFFu) - (pab & 0xFFFFu); // sum_{c > t} cnt[c]
-    const uint32_t vbsum = (tab >> 16) - (pab >> 16);     // sum_{c > t} (cnt[c] + vbacc[c])
-#endif
     uint32_t key = 0xFFFFFFFFu;
     if (t < maxb)
     {
@@ -469,10 +435,6 @@ __device__ __forceinline__ void zero_image(uint32_t * img, uint32_t n16, uint32_
         reinterpret_cast<u32x4 *>(img)[i] = u32x4{0u, 0u, 0u, 0u};
 }
 
-// interior 16-byte chunks with non-temporal stores (A/B knob)
-#ifndef TPF_ENC_STORE_NT
-#define TPF_ENC_STORE_NT 0
-#endif
 __device__ __forceinline__ void copy_out_image16(const uint32_t * img, uint32_t sb, uint64_t dst, uint32_t size, uint64_t cap_end,
                                                  uint32_t t)
 {
@@ -498,11 +460,7 @@ __device__ __forceinline__ void copy_out_image16(const uint32_t * img, uint32_t 
             const uint32_t w0 = img[q], w1 = img[q + 1], w2 = img[q + 2], w3 = img[q + 3], w4 = img[q + 4];
             const u32x4 c = u32x4{__builtin_amdgcn_alignbyte(w1, w0, bs), __builtin_amdgcn_alignbyte(w2, w1, bs),
                                   __builtin_amdgcn_alignbyte(w3, w2, bs), __builtin_amdgcn_alignbyte(w4, w3, bs)};
-#if TPF_ENC_STORE_NT
-            __builtin_nontemporal_store(c, (gu32x4 *)(a16 + 16u * k));
-#else
             *(gu32x4 *)(a16 + 16u * k) = c;
-#endif
         }
         const uint32_t last = (end - 1u) >> 4; // chunk holding the block's last byte
         const uint32_t k = t < 16u ? 0u : last;
@@ -519,34 +477,5 @@ __device__ __forceinline__ void copy_out_image16(const uint32_t * img, uint32_t 
     }
 }
 
-
-// Copy a block built in an LDS image (block byte 0 at image byte sb >= 4) to
-// dst with dword stores: destination dword d of a0 = dst & ~3 holds image
-// bytes base + 4d .. (base = sb - (dst & 3)), realigned by v_alignbyte; the
-// first and last dwords, shared with the neighbouring blocks, byte by byte.
-// (The C1 encoder measured this 9% faster than 16-byte chunks with byte-store
-// edges: an edge costs at most 3 byte stores per side instead of 15.)
-__device__ __forceinline__ void copy_out_dw(const uint32_t * img, uint32_t sb, uint64_t dst, uint32_t size, uint64_t cap_end, uint32_t t)
-{
-    typedef __attribute__((address_space(1))) uint32_t gu32;
-    typedef __attribute__((address_space(1))) uint8_t gu8;
-    const uint32_t ph = static_cast<uint32_t>(dst & 3u);
-    const uint32_t base = sb - ph, qb = base >> 2, bs = base & 3u;
-    const uint64_t a0 = dst & ~3ull;
-    const uint32_t end = ph + size;
-    const uint32_t nd = (end + 3u) >> 2;
-    for (uint32_t d = t; d < nd; d += 64u)
-    {
-        const uint32_t w = __builtin_amdgcn_alignbyte(img[qb + d + 1u], img[qb + d], bs);
-        const uint64_t ga = a0 + 4u * d;
-        const uint32_t lo = 4u * d;
-        if (lo >= ph && lo + 4u <= end && ga + 4u <= cap_end)
-            *(gu32 *)ga = w;
-        else
-            for (uint32_t x = 0; x < 4; ++x)
-                if (lo + x >= ph && lo + x < end && ga + x < cap_end)
-                    *(gu8 *)(ga + x) = static_cast<uint8_t>(w >> (8u * x));
-    }
-}
 
 } // namespace tpf::dev

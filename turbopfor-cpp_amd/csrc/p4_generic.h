@@ -145,12 +145,9 @@ __device__ __forceinline__ uint32_t vbyte_len(uint32_t m)
 // NPOS: scratch entries of scr and of tmp (256; 128 for the 128-value 64-bit
 // blocks, whose valid positions and exception counts are < 128: a malformed
 // position past them is dropped and flagged with kWidthBad)
-// 64-bit vbyte scratch cleared by one 16-byte store per lane instead of two
-// 8-byte stores (A/B knob; round 4, profiles/r4y_d64_ab.txt: C3 64-bit lists
-// +2.5%, C4's 64-bit leg level)
-#ifndef TPF_VBZ16
-#define TPF_VBZ16 1
-#endif
+// The 64-bit vbyte scratch is cleared by one 16-byte store per lane instead
+// of two 8-byte stores (round 4, profiles/r4y_d64_ab.txt: C3 64-bit lists
+// +2.5%, C4's 64-bit leg level).
 template <bool Wide, uint32_t NPOS = 256>
 __device__ __forceinline__ uint32_t vbyte_exceptions_g(const uint32_t * lds, uint32_t v0, uint32_t xn,
                                                        typename std::conditional<Wide, uint64_t, uint32_t>::type * scr,
@@ -160,7 +157,6 @@ __device__ __forceinline__ uint32_t vbyte_exceptions_g(const uint32_t * lds, uin
     using T = typename std::conditional<Wide, uint64_t, uint32_t>::type;
     static_assert(NPOS == 128u || NPOS == 256u, "scratch of 128 or 256 positions");
     constexpr uint32_t PM = NPOS - 1u;
-#if TPF_VBZ16
     // one 16-byte store per lane clears the 64-bit decoder's 1 KB scr
     // (16-byte aligned: k_dec128v64w's scratch, k_dsum128v64_lanes' window)
     if constexpr (Wide && NPOS == 128u)
@@ -169,7 +165,6 @@ __device__ __forceinline__ uint32_t vbyte_exceptions_g(const uint32_t * lds, uin
         reinterpret_cast<z4 *>(scr)[t] = z4{0u, 0u, 0u, 0u};
     }
     else
-#endif
         for (uint32_t i = t; i < NPOS; i += 64u)
             scr[i] = 0;
     wave_lds_sync();
@@ -516,7 +511,7 @@ __device__ __forceinline__ PlanG plan_block_g(const typename FmtTraits<F>::T v[4
     }
     wave_lds_sync();
     uint32_t ec, vbsum;
-    if constexpr (!wide && TPF_PLAN_SUFFIX_LDS)
+    if constexpr (!wide)
     {
         // as plan_block256: suffix sums S(k), the shifted ones through LDS
         const uint32_t incl = wave_incl_scan(cnt);

@@ -133,13 +133,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void k_de
 // The length check is lane-held: one compare and one ballot per run.
 // Reference: src/scalar/p4dec32.cpp:70-142 (p4Dec32), p4d1dec32.cpp.
 constexpr uint32_t kHRun = 64;   // blocks per wave
-// store cache policy of the values (A/B knob).  A block's 508 B start at any
+// store cache policy of the values: default.  A block's 508 B start at any
 // dword, so a store instruction covers parts of three 128-B lines: default
 // write-back stores let L2 merge them (C1, A/B on one box: 900-907 G int32/s)
 // where nt stores ran 632-659 and "sc1 nt" (write-through) 412-416.
-#ifndef TPF_H32_STORE_AUX
-#define TPF_H32_STORE_AUX 0
-#endif
 constexpr uint32_t kHWin = 2560; // window staging bytes per wave (p4Enc32 blocks of n <= 256 values are about 1 KB at most)
 
 // lane-parsed header word: [0,12) payload byte in the window (vbyte: block
@@ -337,7 +334,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
             {
                 const uint32_t el = t + 64u * j;
                 if (j < EPL)
-                    __builtin_amdgcn_raw_buffer_store_b32(v[j], ors, static_cast<int>(el < n ? (jj * n + el) * 4u : 0x80000000u), 0, TPF_H32_STORE_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b32(v[j], ors, static_cast<int>(el < n ? (jj * n + el) * 4u : 0x80000000u), 0, 0);
             }
         }
         wave_lds_sync(); // the next window overwrites the slot
@@ -351,12 +348,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_wav
 }
 
 // ---- run-pipelined encode for the one-block units ------------------------
-// A/B knob: 1 = copy a unit out with 16-byte stores and byte-store edges
-// (copy_out_image16) instead of the dword loop.  C1 encode, one box: 314 vs
-// 342 G int32/s for the dword loop -- kept at 0.
-#ifndef TPF_GENC_COPY16
-#define TPF_GENC_COPY16 0
-#endif
+// Copy-out: a dword loop.  Copying a unit out with 16-byte stores and
+// byte-store edges (copy_out_image16) instead: C1 encode, one box, 314 vs 342
+// G int32/s for the dword loop -- not kept.
 // Plan -> scan -> write as the 256v32 encoder; every wave owns a
 // contiguous run of kGRun units whose values arrive through one buffer
 // descriptor with the next NC-1 units in flight (the first version, one unit
@@ -479,18 +473,6 @@ __global__ __launch_bounds__(256) TPF_SGPR_ATTR void k_enc_gr(const typename Fmt
             const uint64_t o = (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ohi), static_cast<int>(jj)))) << 32)
                              | static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(olo), static_cast<int>(jj)));
             const uint64_t dst = out_base + o;
-#if TPF_GENC_COPY16
-            // the block at image byte 16 + (dst & 15): copy_out_image16 (p4_enc32.h)
-            // writes whole 16-byte chunks and the two edge chunks byte by byte
-            // (the dword loop it replaced took a byte loop on its edge lanes)
-            const uint32_t s0 = 16u + static_cast<uint32_t>(dst & 15u);
-            emit_block_g<F>(img, s0, P, U.v, n, t);
-            wave_lds_sync();
-            copy_out_image16(img, s0, dst, size, cap_end, t);
-            wave_lds_sync();
-            zero_image(img, (s0 + size + 15u) >> 4, t);
-            wave_lds_sync();
-#else
             const uint32_t phase = static_cast<uint32_t>(dst & 3u);
             emit_block_g<F>(img, phase, P, U.v, n, t);
             wave_lds_sync();
@@ -521,7 +503,6 @@ __global__ __launch_bounds__(256) TPF_SGPR_ATTR void k_enc_gr(const typename Fmt
             for (uint32_t d = t; d < nd; d += 64u)
                 img[d] = 0u;
             wave_lds_sync();
-#endif
         }
     };
     if constexpr (WRITE)

@@ -82,9 +82,7 @@ struct RunScanWs
 // pre[r] = sum of tot[0..r) within r's tile, tile[k] = sum of the tiles
 // before k (so run_base = tile[r / kScanTile] + pre[r]); *total (optional) =
 // sum of all run totals.  T = uint64_t: byte offsets; uint32_t: sums mod 2^32.
-// gate (optional): the kernels run only if *gate != 0 (p4_enc256v32.hip's fallback).
-hipError_t launch_run_scan_u64(const uint32_t * tot, uint64_t nruns, uint64_t * pre, uint64_t * tile, uint64_t * total, hipStream_t s,
-                               const uint32_t * gate = nullptr);
+hipError_t launch_run_scan_u64(const uint32_t * tot, uint64_t nruns, uint64_t * pre, uint64_t * tile, uint64_t * total, hipStream_t s);
 hipError_t launch_run_scan_u32(const uint32_t * tot, uint64_t nruns, uint32_t * pre, uint32_t * tile, uint32_t * total, hipStream_t s);
 // u64 run totals (the 64-bit chained decode's unit sums, mod 2^64)
 hipError_t launch_run_scan_u64t(const uint64_t * tot, uint64_t nruns, uint64_t * pre, uint64_t * tile, uint64_t * total, hipStream_t s);

@@ -27,18 +27,11 @@ __device__ __forceinline__ T readlane_t(T x, uint32_t l)
 // Tile k = run totals [k*4096, (k+1)*4096): thread i sums its 16 consecutive
 // entries serially, the 256 thread sums are scanned (wave scans + 4 wave
 // totals in LDS); pre[] = exclusive prefix inside the tile, tile[k] = total.
-__device__ __forceinline__ bool scan_gated_off(const uint32_t * gate)
-{
-    return gate != nullptr && __hip_atomic_load(const_cast<uint32_t *>(gate), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
-}
-
 template <class T, class TT>
 __global__ __launch_bounds__(256) void k_run_scan_tiles(const TT * __restrict tot, uint64_t nruns, T * __restrict pre,
-                                                         T * __restrict tile, const uint32_t * gate)
+                                                         T * __restrict tile)
 {
     __shared__ T wsum[4];
-    if (scan_gated_off(gate))
-        return;
     const uint32_t t = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kScanTile + 16u * threadIdx.x;
     T v[16];
@@ -69,11 +62,9 @@ __global__ __launch_bounds__(256) void k_run_scan_tiles(const TT * __restrict to
 // One workgroup: exclusive scan of the tile totals in place, 1024 per step
 // with a running carry; *total = the sum of everything.
 template <class T>
-__global__ __launch_bounds__(1024) void k_run_scan_tops(T * __restrict tile, uint64_t ntiles, T * __restrict total, const uint32_t * gate)
+__global__ __launch_bounds__(1024) void k_run_scan_tops(T * __restrict tile, uint64_t ntiles, T * __restrict total)
 {
     __shared__ T wsum[16];
-    if (scan_gated_off(gate))
-        return;
     const uint32_t t = threadIdx.x & 63u, w = threadIdx.x >> 6;
     T carry = 0;
     for (uint64_t c = 0; c < ntiles; c += 1024u)
@@ -99,15 +90,6 @@ __global__ __launch_bounds__(1024) void k_run_scan_tops(T * __restrict tile, uin
         *total = carry;
 }
 
-// test hook: base[r] = tile[r / kScanTile] + pre[r]
-__global__ __launch_bounds__(256) void k_run_scan_combine(const uint64_t * __restrict pre, const uint64_t * __restrict tile, uint64_t nruns,
-                                                          uint64_t * __restrict base)
-{
-    const uint64_t r = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
-    if (r < nruns)
-        base[r] = run_base(pre, tile, r);
-}
-
 } // namespace tpf::dev
 
 namespace tpf
@@ -116,24 +98,23 @@ namespace tpf
 namespace
 {
 template <class T, class TT = uint32_t>
-hipError_t run_scan(const TT * tot, uint64_t nruns, T * pre, T * tile, T * total, hipStream_t s, const uint32_t * gate = nullptr)
+hipError_t run_scan(const TT * tot, uint64_t nruns, T * pre, T * tile, T * total, hipStream_t s)
 {
     if (nruns == 0)
         return total ? fill_u32(total, 0u, sizeof(T) / 4u, s) : hipSuccess;
     const uint64_t ntiles = RunScanWs<T>::tiles(nruns);
-    hipLaunchKernelGGL((dev::k_run_scan_tiles<T, TT>), dim3(static_cast<uint32_t>(ntiles)), dim3(256), 0, s, tot, nruns, pre, tile, gate);
+    hipLaunchKernelGGL((dev::k_run_scan_tiles<T, TT>), dim3(static_cast<uint32_t>(ntiles)), dim3(256), 0, s, tot, nruns, pre, tile);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return e;
-    hipLaunchKernelGGL(dev::k_run_scan_tops<T>, dim3(1), dim3(1024), 0, s, tile, ntiles, total, gate);
+    hipLaunchKernelGGL(dev::k_run_scan_tops<T>, dim3(1), dim3(1024), 0, s, tile, ntiles, total);
     return hipGetLastError();
 }
 } // namespace
 
-hipError_t launch_run_scan_u64(const uint32_t * tot, uint64_t nruns, uint64_t * pre, uint64_t * tile, uint64_t * total, hipStream_t s,
-                               const uint32_t * gate)
+hipError_t launch_run_scan_u64(const uint32_t * tot, uint64_t nruns, uint64_t * pre, uint64_t * tile, uint64_t * total, hipStream_t s)
 {
-    return run_scan<uint64_t>(tot, nruns, pre, tile, total, s, gate);
+    return run_scan<uint64_t>(tot, nruns, pre, tile, total, s);
 }
 
 hipError_t launch_run_scan_u64t(const uint64_t * tot, uint64_t nruns, uint64_t * pre, uint64_t * tile, uint64_t * total, hipStream_t s)
@@ -144,24 +125,6 @@ hipError_t launch_run_scan_u64t(const uint64_t * tot, uint64_t nruns, uint64_t *
 hipError_t launch_run_scan_u32(const uint32_t * tot, uint64_t nruns, uint32_t * pre, uint32_t * tile, uint32_t * total, hipStream_t s)
 {
     return run_scan<uint32_t>(tot, nruns, pre, tile, total, s);
-}
-
-size_t test_run_scan_workspace(uint64_t nruns) { return RunScanWs<uint64_t>::bytes(nruns); }
-
-hipError_t test_run_scan(const uint32_t * tot, uint64_t nruns, uint64_t * base, uint64_t * total, void * ws, size_t ws_bytes, hipStream_t s)
-{
-    if (ws_bytes < test_run_scan_workspace(nruns))
-        return hipErrorInvalidValue;
-    const RunScanWs<uint64_t> w = RunScanWs<uint64_t>::carve(ws, nruns);
-    hipError_t e = hipMemcpyAsync(w.tot, tot, 4u * nruns, hipMemcpyDeviceToDevice, s);
-    if (e != hipSuccess)
-        return e;
-    e = run_scan<uint64_t>(w.tot, nruns, w.pre, w.tile, total, s);
-    if (e != hipSuccess || nruns == 0)
-        return e;
-    hipLaunchKernelGGL(dev::k_run_scan_combine, dim3(static_cast<uint32_t>((nruns + 255u) / 256u)), dim3(256), 0, s, w.pre, w.tile, nruns,
-                       base);
-    return hipGetLastError();
 }
 
 } // namespace tpf

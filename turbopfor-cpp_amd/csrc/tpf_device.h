@@ -38,14 +38,7 @@ __device__ __forceinline__ uint64_t uni64(uint64_t x)
 // 83-106.  A cap of 80 (a few SGPRs spill to VGPR lanes): C1 encode 344-346
 // -> 356-358 G int32/s; on the 256v32 writer (86) it was neutral
 // (profiles/r3_enc_sgpr_cap_ab.txt).
-#ifndef TPF_SGPR_CAP
-#define TPF_SGPR_CAP 80
-#endif
-#if TPF_SGPR_CAP
-#define TPF_SGPR_ATTR __attribute__((amdgpu_num_sgpr(TPF_SGPR_CAP)))
-#else
-#define TPF_SGPR_ATTR
-#endif
+#define TPF_SGPR_ATTR __attribute__((amdgpu_num_sgpr(80)))
 
 // Integer min (HIP's min<uint64_t> can resolve to a double overload).
 __device__ __forceinline__ uint64_t min_u64(uint64_t a, uint64_t b) { return a < b ? a : b; }

@@ -55,8 +55,6 @@ struct ServerReq;
 struct ServerAns;
 struct ServerCtl;
 hipError_t launch_block_server(ServerReq * d_req, ServerAns * d_ans, ServerCtl * d_ctl, hipStream_t s);
-// Measurement only: streaming read / write / copy ceilings (hbm_probe.hip).
-hipError_t launch_probe_hbm(int kind, void * dst, const void * src, uint64_t bytes, hipStream_t s);
 
 // (fmt, n) accepted by the batch entry points (capi.cpp)
 bool fmt_ok(int fmt, unsigned n);
@@ -70,12 +68,8 @@ hipError_t launch_enc_generic(int fmt, const void * in, uint64_t nblocks, uint32
 hipError_t launch_dec256v32(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * out,
                             const uint32_t * starts, unsigned long long * err, hipStream_t stream);
 
-hipError_t launch_probe256v32(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, uint32_t * out,
-                              hipStream_t stream);
 
 // run scan test hook (p4_scan.hip)
-size_t test_run_scan_workspace(uint64_t nruns);
-hipError_t test_run_scan(const uint32_t * tot, uint64_t nruns, uint64_t * base, uint64_t * total, void * ws, size_t ws_bytes, hipStream_t s);
 size_t d1chain_workspace(uint64_t nblocks);
 hipError_t launch_d1chain_sums(const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nblocks, void * ws, size_t ws_bytes,
                                uint32_t * total, unsigned long long * err, hipStream_t stream);
@@ -84,8 +78,6 @@ hipError_t launch_d1chain_decode(const uint8_t * in, uint64_t in_bytes, const ui
 
 hipError_t launch_dec128v64(uint32_t nb, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nunits,
                             uint64_t * out, const uint64_t * starts, unsigned long long * err, hipStream_t s);
-hipError_t launch_probe128v64(uint32_t nb, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nunits, uint64_t * out,
-                              hipStream_t s);
 
 size_t d1chain64_workspace(uint64_t nunits);
 hipError_t launch_d1chain64_sums(uint32_t nb, const uint8_t * in, uint64_t in_bytes, const uint64_t * off, uint64_t nunits, void * ws,
@@ -99,7 +91,6 @@ hipError_t launch_enc128v64(uint32_t nb, const uint64_t * in, uint64_t nunits, b
 
 size_t enc256v32_workspace(uint64_t nblocks);
 hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, bool d1,
-                            uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t stream,
-                            int probe = 0);
+                            uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t stream);
 
 } // namespace tpf

@@ -1,5 +1,5 @@
-// hbm_probe.hip -- measurement-only streaming kernels (no reference
-// counterpart): the box's own HBM ceilings, timed inside bench.py in the same
+// hbm_probe.hip -- measurement-library streaming kernels (no reference
+// counterpart; not in the codec library): the box's own HBM ceilings, timed inside bench.py in the same
 // process as the codec so the line's "ceiling" numbers are measured in-run.
 //
 //   kind 0  read : every lane XOR-folds 16-byte non-temporal loads (a sink
@@ -12,8 +12,9 @@
 // profiles/archive/r1/r1_v3_hbm_probes.txt).
 #include <hip/hip_runtime.h>
 
-#include "tpf_device.h"
-#include "tpf_kernels.h"
+#include "../csrc/tpf_device.h"
+#include "../csrc/tpf_kernels.h"
+#include "tpf_measure.h"
 
 namespace tpf::dev
 {
@@ -45,11 +46,13 @@ __global__ __launch_bounds__(256) void k_probe_copy(const u32x4 * __restrict__ a
 
 } // namespace tpf::dev
 
-namespace tpf
+namespace tpfm
 {
 
 hipError_t launch_probe_hbm(int kind, void * dst, const void * src, uint64_t bytes, hipStream_t s)
 {
+    using tpf::grid_cap;
+    namespace dev = tpf::dev;
     const uint64_t n = bytes / 16u;
     if (n == 0)
         return hipSuccess;
@@ -73,4 +76,4 @@ hipError_t launch_probe_hbm(int kind, void * dst, const void * src, uint64_t byt
     return hipGetLastError();
 }
 
-} // namespace tpf
+} // namespace tpfm

@@ -1,0 +1,126 @@
+// tpf_measure.hip -- the measurement and test library (tpf_measure.h): the
+// kernels' data-movement probes, forced encoder paths and the run-scan test
+// hook, instantiated from the codec's own kernel headers so each probe runs
+// the exact loads and stores of the kernel it measures.  Nothing here is
+// reachable from libturbopfor_amd.so.
+#include <hip/hip_runtime.h>
+
+#include "../csrc/p4_dec256v32.h"
+#include "../csrc/p4_dec256v64.h"
+#include "../csrc/p4_enc256v32.h"
+#include "tpf_measure.h"
+
+namespace tpfm
+{
+hipError_t launch_probe_hbm(int kind, void * dst, const void * src, uint64_t bytes, hipStream_t s); // hbm_probe.hip
+
+namespace dev
+{
+// test hook: base[r] = tile[r / kScanTile] + pre[r]
+__global__ __launch_bounds__(256) void k_run_scan_combine(const uint64_t * __restrict pre, const uint64_t * __restrict tile, uint64_t nruns,
+                                                          uint64_t * __restrict base)
+{
+    const uint64_t r = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+    if (r < nruns)
+        base[r] = tpf::dev::run_base(pre, tile, r);
+}
+} // namespace dev
+
+int rc(hipError_t e) { return e == hipSuccess ? 0 : static_cast<int>(e); }
+
+} // namespace tpfm
+
+extern "C" {
+
+int tpfm_probe256v32(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nblocks, uint32_t * d_out, void * stream)
+{
+    namespace dev = tpf::dev;
+    if (nblocks == 0)
+        return 0;
+    if (!d_in || !d_off || !d_out)
+        return -1;
+    const dev::DecArgs A{d_in, in_bytes, d_off, nblocks, d_out, nullptr, 0u, nullptr, nullptr};
+    constexpr uint32_t run = dev::kRunDefault;
+    const uint32_t grid = static_cast<uint32_t>((nblocks + 4ull * run - 1) / (4ull * run));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // the same per-launch choice as the library's plain decode (p4_dec256v32.hip)
+    if (dev::dec_grouped(in_bytes, nblocks))
+        hipLaunchKernelGGL((dev::k_dec256v32w<dev::StartMode::Probe, run, dev::kDecPol, dev::kDecNC, dev::kDecMinW, true, 1024u>), dim3(grid),
+                           dim3(256), 0, s, A);
+    else
+        hipLaunchKernelGGL((dev::k_dec256v32w<dev::StartMode::Probe, run, dev::kDecPol, dev::kDecNC, dev::kDecMinW, true, 0u>), dim3(grid),
+                           dim3(256), 0, s, A);
+    return tpfm::rc(hipGetLastError());
+}
+
+int tpfm_probe256v64(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nunits, uint64_t * d_out, void * stream)
+{
+    namespace dev = tpf::dev;
+    if (nunits == 0)
+        return 0;
+    if (!d_in || !d_off || !d_out)
+        return -1;
+    const dev::Dec64Args A{d_in, in_bytes, d_off, nunits, d_out, nullptr, 0ull, nullptr, nullptr, nullptr, nullptr, nullptr};
+    const uint32_t grid = static_cast<uint32_t>((nunits + 4u * dev::kRun64 - 1u) / (4u * dev::kRun64));
+    hipLaunchKernelGGL((dev::k_dec128v64w<2, dev::Start64::Probe>), dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), A);
+    return tpfm::rc(hipGetLastError());
+}
+
+int tpfm_probe_hbm(int kind, void * d_dst, const void * d_src, uint64_t bytes, void * stream)
+{
+    if (kind < 0 || kind > 2 || !d_dst || (kind != 1 && !d_src))
+        return -1;
+    return tpfm::rc(tpfm::launch_probe_hbm(kind, d_dst, d_src, bytes, static_cast<hipStream_t>(stream)));
+}
+
+int tpfm_enc256v32(int mode, const uint32_t * d_in, uint64_t nblocks, int d1, const uint32_t * d_starts, uint32_t start0, uint8_t * d_out,
+                   uint64_t out_cap, uint64_t * d_off, void * d_ws, size_t ws_bytes, void * stream)
+{
+    namespace enc256 = tpf::enc256;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (!d_off || (nblocks && (!d_in || !d_out || !d_ws)))
+        return -1;
+    if (nblocks == 0)
+        return tpfm::rc(tpf::fill_u32(d_off, 0u, 2, s));
+    if (nblocks + 1 > 0x7FFFFFFFull || ws_bytes < enc256::twopass_workspace(nblocks) || out_cap < nblocks * 1800u + 64u)
+        return -1;
+    switch (mode)
+    {
+        case 1:
+            return d1 ? -1 : tpfm::rc(enc256::launch_twopass<1, 0>(d_in, nblocks, nullptr, 0u, false, d_out, out_cap, d_off, d_ws, s));
+        case 2:
+            return d1 ? -1 : tpfm::rc(enc256::launch_twopass<0, 2>(d_in, nblocks, nullptr, 0u, false, d_out, out_cap, d_off, d_ws, s));
+        case 3:
+            return tpfm::rc(enc256::launch_twopass<0, 0>(d_in, nblocks, d_starts, start0, d1 != 0, d_out, out_cap, d_off, d_ws, s));
+        case 4:
+            if (ws_bytes < enc256::slot_workspace(nblocks))
+                return -1;
+            return tpfm::rc(enc256::launch_slot(d_in, nblocks, d_starts, start0, d1 != 0, d_out, out_cap, d_off, d_ws, s));
+        default:
+            return -1;
+    }
+}
+
+size_t tpfm_run_scan_workspace_size(uint64_t nruns) { return tpf::RunScanWs<uint64_t>::bytes(nruns); }
+
+int tpfm_run_scan(const uint32_t * d_tot, uint64_t nruns, uint64_t * d_base, uint64_t * d_total, void * d_ws, size_t ws_bytes, void * stream)
+{
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (ws_bytes < tpfm_run_scan_workspace_size(nruns) || (nruns && (!d_tot || !d_base || !d_ws)))
+        return -1;
+    const tpf::RunScanWs<uint64_t> w = tpf::RunScanWs<uint64_t>::carve(d_ws, nruns);
+    if (nruns)
+    {
+        hipError_t e = hipMemcpyAsync(w.tot, d_tot, 4u * nruns, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess)
+            return tpfm::rc(e);
+    }
+    hipError_t e = tpf::launch_run_scan_u64(w.tot, nruns, w.pre, w.tile, d_total, s);
+    if (e != hipSuccess || nruns == 0)
+        return tpfm::rc(e);
+    hipLaunchKernelGGL(tpfm::dev::k_run_scan_combine, dim3(static_cast<uint32_t>((nruns + 255u) / 256u)), dim3(256), 0, s, w.pre, w.tile,
+                       nruns, d_base);
+    return tpfm::rc(hipGetLastError());
+}
+
+} // extern "C"

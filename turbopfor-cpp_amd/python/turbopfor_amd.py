@@ -81,9 +81,6 @@ def lib():
         L.tpf_device_count.restype = ctypes.c_int
         L.tpf_p4dec256v32_batch.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp, c_vp]
         L.tpf_p4d1dec256v32_batch.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp, c_vp, c_vp]
-        L.tpf_probe256v32.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp]
-        L.tpf_probe_hbm.argtypes = [ctypes.c_int, c_vp, c_vp, c_u64, c_vp]
-        L.tpf_probe_enc256v32.argtypes = [ctypes.c_int, c_vp, c_u64, c_vp, c_u64, c_vp, c_vp, ctypes.c_size_t, c_vp]
         L.tpf_p4enc256v32_bound.argtypes = [c_u64]
         L.tpf_p4enc256v32_bound.restype = c_u64
         L.tpf_p4enc256v32_workspace_size.argtypes = [c_u64]
@@ -123,13 +120,9 @@ def lib():
             L.tpf_d1dec64_chain_decode.argtypes = [ctypes.c_int, c_vp, c_u64, c_vp, c_u64, c_vp, c_u64, c_vp, c_vp, c_vp]
             for name in ("tpf_d1dec64_chained", "tpf_d1dec64_chain_sums", "tpf_d1dec64_chain_decode"):
                 getattr(L, name).restype = ctypes.c_int
-        if hasattr(L, "tpf_probe256v64"):
-            L.tpf_probe256v64.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp]
-            L.tpf_probe256v64.restype = ctypes.c_int
         for name in ("tpf_p4nenc256v32", "tpf_p4ndec256v32", "tpf_p4dec256v32_batch", "tpf_p4d1dec256v32_batch", "tpf_p4enc256v32_batch",
                      "tpf_p4d1enc256v32_batch", "tpf_dec_batch", "tpf_enc_batch", "tpf_p4d1dec256v32_chained",
-                     "tpf_p4d1dec256v32_chain_sums", "tpf_p4d1dec256v32_chain_decode", "tpf_probe256v32",
-                     "tpf_probe_hbm", "tpf_probe_enc256v32"):
+                     "tpf_p4d1dec256v32_chain_sums", "tpf_p4d1dec256v32_chain_decode"):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -168,12 +161,47 @@ def dec256v32(packed, offsets, nblocks, out=None, starts=None, err=None):
     return out
 
 
+# ---- the measurement / test library (measure/tpf_measure.h) --------------
+# Not the codec: kernel probes, device ceilings, forced encoder paths and the
+# run-scan test hook, loaded only by bench.py, the GPU tests and scripts/.
+MEASURE_PATH = os.path.join(PKG_DIR, "lib", "libtpf_measure.so")
+_mlib = None
+
+
+def measure():
+    """Load lib/libtpf_measure.so (after the codec library it links)."""
+    global _mlib
+    if _mlib is None:
+        lib()
+        if not os.path.exists(MEASURE_PATH):
+            build()
+        M = ctypes.CDLL(MEASURE_PATH)
+        M.tpfm_probe256v32.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp]
+        M.tpfm_probe256v64.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp]
+        M.tpfm_probe_hbm.argtypes = [ctypes.c_int, c_vp, c_vp, c_u64, c_vp]
+        M.tpfm_enc256v32.argtypes = [ctypes.c_int, c_vp, c_u64, ctypes.c_int, c_vp, ctypes.c_uint32, c_vp, c_u64, c_vp, c_vp,
+                                     ctypes.c_size_t, c_vp]
+        M.tpfm_run_scan_workspace_size.argtypes = [c_u64]
+        M.tpfm_run_scan_workspace_size.restype = ctypes.c_size_t
+        M.tpfm_run_scan.argtypes = [c_vp, c_u64, c_vp, c_vp, c_vp, ctypes.c_size_t, c_vp]
+        for name in ("tpfm_probe256v32", "tpfm_probe256v64", "tpfm_probe_hbm", "tpfm_enc256v32", "tpfm_run_scan"):
+            getattr(M, name).restype = ctypes.c_int
+        _mlib = M
+    return _mlib
+
+
+def _mcheck(rc, what):
+    if rc != 0:
+        raise TpfError(f"{what}: measurement library error {rc}")
+
+
 def probe256v64(packed, offsets, nunits, out):
     """Measurement only: the 256v64 decode kernel's loads and stores without
-    the decoding (tpf_probe256v64)."""
+    the decoding (tpfm_probe256v64)."""
     import torch
 
-    _check(lib().tpf_probe256v64(_ptr(packed), packed.numel(), _ptr(offsets), nunits, _ptr(out), _stream(torch)))
+    _mcheck(measure().tpfm_probe256v64(_ptr(packed), packed.numel(), _ptr(offsets), nunits, _ptr(out), _stream(torch)),
+            "tpfm_probe256v64")
     return out
 
 
@@ -182,33 +210,33 @@ def probe256v32(packed, offsets, nblocks, out):
     decoding (data-movement ceiling of the hot path's access pattern)."""
     import torch
 
-    _check(lib().tpf_probe256v32(_ptr(packed), packed.numel(), _ptr(offsets), nblocks, _ptr(out), _stream(torch)))
+    _mcheck(measure().tpfm_probe256v32(_ptr(packed), packed.numel(), _ptr(offsets), nblocks, _ptr(out), _stream(torch)),
+            "tpfm_probe256v32")
     return out
 
 
 def probe_hbm(kind, dst, src, nbytes):
-    """Measurement only: streaming ceiling kernels (tpf_probe_hbm): kind
+    """Measurement only: streaming ceiling kernels (tpfm_probe_hbm): kind
     "read" (src), "write" (dst) or "copy" (src -> dst) of nbytes bytes."""
     import torch
 
     k = {"read": 0, "write": 1, "copy": 2}[kind]
-    _check(lib().tpf_probe_hbm(k, _ptr(dst), _ptr(src), nbytes, _stream(torch)))
+    _mcheck(measure().tpfm_probe_hbm(k, _ptr(dst), _ptr(src), nbytes, _stream(torch)), "tpfm_probe_hbm")
 
 
-def probe_enc256v32(mode, values, out):
-    """Measurement / test hooks of the 256v32 encoder (tpf_probe_enc256v32):
-    mode 1 = plan pass as a wave OR, 2 = write pass copying values (not a
-    valid stream); 0 / 3 = the two-pass encoder.  Returns the offsets tensor
-    [nblocks+1]."""
+def enc256v32_path(mode, values, out, d1=False, starts=None, start0=0):
+    """The 256v32 encoder through a forced path (tpfm_enc256v32): mode 1 =
+    plan pass as a wave OR, 2 = write pass copying values (plain only, not a
+    valid stream), 3 = the two-pass encoder, 4 = the slot encoder.  Returns
+    the offsets tensor [nblocks+1]."""
     import torch
 
     nb = values.numel() // 256
-    L = lib()
     offs = torch.empty(nb + 1, dtype=torch.int64, device=values.device)
-    ws_bytes = int(L.tpf_p4enc256v32_workspace_size(nb))
+    ws_bytes = int(lib().tpf_p4enc256v32_workspace_size(nb))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=values.device)
-    _check(L.tpf_probe_enc256v32(mode, _ptr(values), nb, _ptr(out), out.numel(), _ptr(offs), _ptr(ws), ws_bytes,
-                                 _stream(torch)))
+    _mcheck(measure().tpfm_enc256v32(mode, _ptr(values), nb, 1 if d1 else 0, _ptr(starts), ctypes.c_uint32(start0 & 0xFFFFFFFF),
+                                     _ptr(out), out.numel(), _ptr(offs), _ptr(ws), ws_bytes, _stream(torch)), "tpfm_enc256v32")
     return offs
 
 
