@@ -157,13 +157,14 @@ def test_full_size_c3_sample_vs_oracle():
     assert torch.equal(out2, vals)
 
 
-@pytest.mark.parametrize("mode", [0, 3, 4])
+@pytest.mark.parametrize("mode", [0, 3, 4, 5])
 @pytest.mark.parametrize("nb", [1, 15, 16, 17, 31, 33, 1000, 20_000])
 def test_encoder_entries_vs_oracle(mode, nb):
     """The 256v32 encoder through the batch entry (mode 0, the library's own
     choice of path) and both paths forced through the measurement library
     (tpfm_enc256v32): 3 = two-pass (plan, run scan, write), 4 = slot (plan +
-    build into per-run slots, run scan, compaction).  Byte-exact vs the
+    build into per-run slots, run scan, compaction), 5 = slot without the
+    fused plan/build scans.  Byte-exact vs the
     oracle, mixed widths and exception rates, ragged last runs (a run is 16
     blocks)."""
     blocks = mixed_blocks(nb, nb + mode)
@@ -181,7 +182,7 @@ def test_encoder_entries_vs_oracle(mode, nb):
     np.testing.assert_array_equal(packed, exp_packed)
 
 
-@pytest.mark.parametrize("mode", [3, 4])
+@pytest.mark.parametrize("mode", [3, 4, 5])
 @pytest.mark.parametrize("chained", [True, False])
 def test_encoder_paths_d1_vs_oracle(mode, chained):
     """p4D1Enc256v32 through both forced paths, one chained C3 list (start0 +

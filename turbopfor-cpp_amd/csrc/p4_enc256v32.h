@@ -280,7 +280,7 @@ __global__ __launch_bounds__(256) void k_enc256v32_write(const uint32_t * __rest
 // b = 32: 16 x 1025 B), so the workspace is ~1.03x the input.
 constexpr uint32_t kSlotRunBytes = 16512; // >= 16 x 1025, a multiple of 128
 
-template <bool D1>
+template <bool D1, bool FUSE>
 __global__ __launch_bounds__(256) void k_enc256v32_slot(const uint32_t * __restrict in, uint64_t nblocks,
                                                          const uint32_t * __restrict starts, uint32_t start0,
                                                          uint64_t * __restrict sizes, uint32_t * __restrict run_tot,
@@ -308,9 +308,10 @@ __global__ __launch_bounds__(256) void k_enc256v32_slot(const uint32_t * __restr
                 v = delta_encode(v, rl32(stv, jj), t);
             // the histogram (plan) and the staged values (build) share `val`:
             // the plan has read its bins back before the build stages values
-            const Plan32 P = plan_block256(v, val, t);
+            VbPre pre;
+            const Plan32 P = plan_block256<FUSE>(v, val, t, &pre);
             wave_lds_sync();
-            const uint32_t sb = emit_block256<true>(img, val, P, v, t);
+            const uint32_t sb = emit_block256<true, FUSE>(img, val, P, v, t, &pre);
             wave_lds_sync();
             copy_out_image16(img, sb, slot + pos, P.size, ~0ull, t);
             wave_lds_sync();
@@ -398,6 +399,7 @@ inline size_t twopass_workspace(uint64_t nblocks) { return al256(nblocks * 4u) +
 inline size_t slot_workspace(uint64_t nblocks) { return twopass_workspace(nblocks) + al256(enc_runs(nblocks) * dev::kSlotRunBytes); }
 
 // plan+build into slots -> run scan -> compact
+template <bool FUSE = true>
 inline hipError_t launch_slot(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, bool d1, uint8_t * out,
                               uint64_t out_cap, uint64_t * off, void * ws, hipStream_t stream)
 {
@@ -407,10 +409,10 @@ inline hipError_t launch_slot(const uint32_t * in, uint64_t nblocks, const uint3
     const uint64_t per_wg = 4ull * dev::kEncRun;
     const uint32_t grid = static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg);
     if (d1)
-        hipLaunchKernelGGL((dev::k_enc256v32_slot<true>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, rs.tot,
+        hipLaunchKernelGGL((dev::k_enc256v32_slot<true, FUSE>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, rs.tot,
                            slots);
     else
-        hipLaunchKernelGGL((dev::k_enc256v32_slot<false>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, rs.tot,
+        hipLaunchKernelGGL((dev::k_enc256v32_slot<false, FUSE>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, rs.tot,
                            slots);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)

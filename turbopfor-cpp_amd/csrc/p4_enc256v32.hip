@@ -27,7 +27,8 @@ static int enc_path()
 
 // The path (round 5): the slot encoder (values read once,
 // p4_enc256v32.h) when the workspace holds the slots, else the two-pass
-// encoder.  TPF_ENC_PATH=1 / 2 forces two-pass / slot (A/B runs).
+// encoder.  TPF_ENC_PATH=1 / 2 / 3 forces two-pass / slot / slot without
+// the fused plan+build scans (A/B runs).
 hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, bool d1,
                             uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t stream)
 {
@@ -37,7 +38,9 @@ hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_
         return hipErrorInvalidValue;
     const bool slot_ok = ws_bytes >= enc256::slot_workspace(nblocks);
     if (slot_ok && enc_path() == 2)
-        return enc256::launch_slot(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream);
+        return enc256::launch_slot<true>(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream);
+    if (slot_ok && enc_path() == 3)
+        return enc256::launch_slot<false>(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream);
     return enc256::launch_twopass<0, 0>(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream);
 }
 

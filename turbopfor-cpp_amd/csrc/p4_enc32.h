@@ -54,7 +54,17 @@ __device__ __forceinline__ uint32_t ffbh1(uint32_t x)
 // 4 copies 453-457; merging equal widths within a lane first: no gain)
 using PlanHist = WaveHist<4, 36>; // bit widths 0..32
 constexpr uint32_t kPlanHistU32 = PlanHist::kU32;
-__device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist, uint32_t t)
+// A vbyte block's exception ranks and byte offsets, computed once by the
+// plan and handed to the build (the slot encoder plans and builds in one
+// wave: FUSE): lane t's exceptions are ranks before.. and their vbytes start
+// at byte lbefore of the vbyte area; vtotal = the area's byte count.
+struct VbPre
+{
+    uint32_t before = 0, lbefore = 0, vtotal = 0;
+};
+
+template <bool FUSE = false>
+__device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist, uint32_t t, VbPre * pre = nullptr)
 {
     Plan32 P;
     const uint32_t orv = uni(wave_or(v.x | v.y | v.z | v.w));
@@ -144,6 +154,25 @@ __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist
     // threshold (compares on the VALU, counts on the scalar unit) instead of a
     // per-value length under exec masks and a wave reduction
     const uint32_t y0 = v.x >> b, y1 = v.y >> b, y2 = v.z >> b, y3 = v.w >> b; // b < maxb <= 32
+    if constexpr (FUSE)
+    {
+        // one wave scan of (exceptions, vbyte bytes) per lane gives the totals
+        // here and the build's ranks and byte offsets (emit_block256<.., true>)
+        const uint32_t f0 = y0 != 0u, f1 = y1 != 0u, f2 = y2 != 0u, f3 = y3 != 0u;
+        const uint32_t mylen = (vblen32(y0) & (0u - f0)) + (vblen32(y1) & (0u - f1)) + (vblen32(y2) & (0u - f2)) + (vblen32(y3) & (0u - f3));
+        const uint32_t mine = (f0 + f1 + f2 + f3) | (mylen << 16); // <= 256 exceptions, <= 1280 bytes: no carry between the halves
+        const uint32_t incl = wave_incl_scan(mine);
+        const uint32_t tot = uni(__builtin_amdgcn_readlane(incl, 63));
+        const uint32_t xn = tot & 0xFFFFu, sumlen = tot >> 16;
+        pre->before = (incl - mine) & 0xFFFFu;
+        pre->lbefore = (incl - mine) >> 16;
+        pre->vtotal = sumlen;
+        P.xn = xn;
+        P.bx = 33;
+        P.raw = (sumlen + 32u > 4u * xn) ? 1u : 0u;
+        P.size = 2u + 32u * b + (P.raw ? 1u + 4u * xn : sumlen) + xn;
+        return P;
+    }
     auto count_ge = [&](uint32_t T) -> uint32_t {
         return static_cast<uint32_t>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(y0 >= T))
                                      + __builtin_popcountll(__builtin_amdgcn_ballot_w64(y1 >= T))
@@ -254,9 +283,9 @@ __device__ __forceinline__ void pack_base_runs(uint32_t * img, uint32_t pw, cons
 
 // Build block image; returns sb (image byte of the block's first byte).
 // v: lane t's values 4t..4t+3 (after delta coding), P: plan, val: scratch.
-template <bool PAD = false>
+template <bool PAD = false, bool FUSE = false>
 __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val, const Plan32 & P, const u32x4 & v,
-                                                  uint32_t t)
+                                                  uint32_t t, const VbPre * pre = nullptr)
 {
     uint8_t * const ib = reinterpret_cast<uint8_t *>(img);
     const uint32_t b = P.b;
@@ -287,8 +316,8 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
     const uint32_t f0 = v.x > m, f1 = v.y > m, f2 = v.z > m, f3 = v.w > m;
     const uint32_t my = f0 | (f1 << 1) | (f2 << 2) | (f3 << 3);
     const uint32_t cnt = f0 + f1 + f2 + f3;
-    const uint32_t incl = wave_incl_scan(cnt);
-    const uint32_t before = incl - cnt; // exceptions in elements < 4t
+    // exceptions in elements < 4t (a fused vbyte plan scanned them already)
+    const uint32_t before = (FUSE && P.bx == 33u) ? pre->before : wave_incl_scan(cnt) - cnt;
     const uint32_t sh = b & 31u;
     const uint32_t ex[4] = {v.x >> sh, v.y >> sh, v.z >> sh, v.w >> sh};
     if (P.bx <= 32u)
@@ -380,13 +409,22 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
         return sb;
     }
     // vbPut32 (p4_scalar_internal.cpp:47-89): byte offsets from a wave scan of the lengths
-    uint32_t mylen = 0u;
+    uint32_t A, vtotal;
+    if constexpr (FUSE)
+    {
+        A = v0 + pre->lbefore;
+        vtotal = pre->vtotal;
+    }
+    else
+    {
+        uint32_t mylen = 0u;
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j)
-        mylen += vblen32(ex[j]) & (0u - ((my >> j) & 1u));
-    const uint32_t lincl = wave_incl_scan(mylen);
-    const uint32_t vtotal = __builtin_amdgcn_readlane(lincl, 63);
-    uint32_t A = v0 + lincl - mylen;
+        for (uint32_t j = 0; j < 4; ++j)
+            mylen += vblen32(ex[j]) & (0u - ((my >> j) & 1u));
+        const uint32_t lincl = wave_incl_scan(mylen);
+        vtotal = __builtin_amdgcn_readlane(lincl, 63);
+        A = v0 + lincl - mylen;
+    }
     const uint32_t pbase = v0 + vtotal;
 #pragma unroll
     for (uint32_t i = 0; i < 4u; ++i)

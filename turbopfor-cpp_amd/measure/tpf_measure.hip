@@ -93,9 +93,11 @@ int tpfm_enc256v32(int mode, const uint32_t * d_in, uint64_t nblocks, int d1, co
         case 3:
             return tpfm::rc(enc256::launch_twopass<0, 0>(d_in, nblocks, d_starts, start0, d1 != 0, d_out, out_cap, d_off, d_ws, s));
         case 4:
+        case 5:
             if (ws_bytes < enc256::slot_workspace(nblocks))
                 return -1;
-            return tpfm::rc(enc256::launch_slot(d_in, nblocks, d_starts, start0, d1 != 0, d_out, out_cap, d_off, d_ws, s));
+            return tpfm::rc(mode == 4 ? enc256::launch_slot<true>(d_in, nblocks, d_starts, start0, d1 != 0, d_out, out_cap, d_off, d_ws, s)
+                                      : enc256::launch_slot<false>(d_in, nblocks, d_starts, start0, d1 != 0, d_out, out_cap, d_off, d_ws, s));
         default:
             return -1;
     }
