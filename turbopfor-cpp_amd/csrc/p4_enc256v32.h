@@ -360,14 +360,32 @@ __global__ __launch_bounds__(256) void k_enc256v32_compact(const uint8_t * __res
         const uint32_t q = static_cast<uint32_t>(16u * c0 - base); // slot byte of chunk c0 (0..15)
         const uint32_t qa = q & ~3u, qs = q & 3u;
         const uint32_t nc = c1 > c0 ? static_cast<uint32_t>(c1 - c0) : 0u;
-        for (uint32_t k = t; k < nc; k += 64u)
+        // four chunks per lane in flight: the loads of a step are issued
+        // together (a chunk past the run reads as zeros from an out-of-range
+        // offset: no traffic), then realigned and stored
+        constexpr uint32_t U = 4;
+        for (uint32_t k0 = 0; k0 < nc; k0 += 64u * U)
         {
-            // slot bytes [q + 16k, q + 16k + 16): dwords from qa + 16k, five of them
-            const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(qa + 16u * k), 0, 0);
-            const uint32_t e = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(qa + 16u * k + 16u), 0, 0);
-            const u32x4 c = u32x4{__builtin_amdgcn_alignbyte(a.y, a.x, qs), __builtin_amdgcn_alignbyte(a.z, a.y, qs),
-                                  __builtin_amdgcn_alignbyte(a.w, a.z, qs), __builtin_amdgcn_alignbyte(e, a.w, qs)};
-            *(gu32x4 *)(o + 16u * (c0 + k)) = c;
+            u32x4 a[U];
+            uint32_t e[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u)
+            {
+                // slot bytes [q + 16k, q + 16k + 16): dwords from qa + 16k, five of them
+                const uint32_t k = k0 + 64u * u + t;
+                const int at = k < nc ? static_cast<int>(qa + 16u * k) : static_cast<int>(0x80000000u);
+                a[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, at, 0, 0);
+                e[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, at + 16, 0, 0);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u)
+            {
+                const uint32_t k = k0 + 64u * u + t;
+                const u32x4 c = u32x4{__builtin_amdgcn_alignbyte(a[u].y, a[u].x, qs), __builtin_amdgcn_alignbyte(a[u].z, a[u].y, qs),
+                                      __builtin_amdgcn_alignbyte(a[u].w, a[u].z, qs), __builtin_amdgcn_alignbyte(e[u], a[u].w, qs)};
+                if (k < nc)
+                    *(gu32x4 *)(o + 16u * (c0 + k)) = c;
+            }
         }
         // partial chunks: head bytes [base, 16 c0), tail bytes [16 c1, end)
         const uint64_t g = t < 16u ? base + t : 16u * c1 + (t - 16u);
