@@ -163,7 +163,8 @@ def test_small_block_grouped_path_vs_oracle(pad, mix):
     packed_np, off_np = oracle_lib.enc256v32_batch(blocks)
     assert len(packed_np) < 300 * len(blocks)
     expect = oracle_lib.dec256v32_batch(packed_np, off_np, len(blocks))
-    packed, offs = to_dev_stream([packed_np.tobytes()], pad_front=pad)
+    packed, _ = to_dev_stream([packed_np.tobytes()], pad_front=pad)
+    offs = torch.from_numpy(off_np.astype(np.int64)).to(DEV)
     err = torch.zeros(1, dtype=torch.int64, device=DEV)
     out = tpf.dec256v32(packed, offs, len(blocks), err=err)
     torch.cuda.synchronize()
@@ -176,3 +177,27 @@ def test_small_block_grouped_path_vs_oracle(pad, mix):
     torch.cuda.synchronize()
     assert int(err.item()) == 776
     assert_blocks_equal(as_u32(out)[:776 * 256], expect[:776], "grouped decode before the corruption")
+
+
+@pytest.mark.parametrize("small", [False, True])
+def test_offsets_outside_the_stream_are_reported_not_followed(small):
+    """Offsets are input too: a block whose offsets leave the stream (past
+    in_bytes, far past it, or ending before they start) loads nothing and is
+    reported through d_err; the decoder never bases a load on them (round 5:
+    a caller passing too short an offset array made the decoder read garbage
+    offsets and fault).  Both pipelines: single-block and grouped (small)."""
+    blocks = datagen.c2_blocks(800, 2 if small else 14, 10, seed=3)
+    packed_np, off_np = oracle_lib.enc256v32_batch(blocks)
+    expect = oracle_lib.dec256v32_batch(packed_np, off_np, len(blocks))
+    packed, _ = to_dev_stream([packed_np.tobytes()])
+    total = int(off_np[-1])
+    for at, bad in ((400, [total + 64, total + 96]), (500, [1 << 40, (1 << 40) + 300]), (600, [2000, 1000]),
+                    (700, [(1 << 64) - 256, (1 << 64) - 16])):
+        o = off_np.astype(np.uint64).copy()
+        o[at], o[at + 1] = bad
+        err = torch.zeros(1, dtype=torch.int64, device=DEV)
+        out = tpf.dec256v32(packed, torch.from_numpy(o.view(np.int64)).to(DEV), len(blocks), err=err)
+        torch.cuda.synchronize()
+        # block at-1 ends at the bad offset: it is the first one reported
+        assert int(err.item()) == at - 1, (at, int(err.item()))
+        assert_blocks_equal(as_u32(out)[:(at - 1) * 256], expect[:at - 1], f"decode before offsets {at}")

@@ -98,14 +98,14 @@ __global__ __launch_bounds__(256, MINW) void k_dec256v32w(const DecArgs A)
     if constexpr (GB != 0u)
     {
         static_assert(ONE && stride == 1u && kRun <= 64u && GB <= 1024u, "groups: one load per lane, contiguous runs");
-        blen = (e >= o && e - o < 0x10000ull) ? static_cast<uint32_t>(e - o) : 0xFFFFFFFFu;
+        blen = (e >= o && e <= A.in_bytes && e - o < 0x10000ull) ? static_cast<uint32_t>(e - o) : 0xFFFFFFFFu;
         const uint64_t ab = in_base + o;
         ablo = static_cast<uint32_t>(ab);
         ng = 0u;
         for (uint32_t j = 0; j < n;)
         {
             const uint64_t cb = readlane_u64(ab, j) & ~15ull;
-            const uint64_t fit = __ballot(valid && t >= j && e >= o && in_base + e <= cb + GB) >> j;
+            const uint64_t fit = __ballot(valid && t >= j && e >= o && e <= A.in_bytes && in_base + e <= cb + GB) >> j;
             uint32_t c = static_cast<uint32_t>(__builtin_ctzll(~fit)); // consecutive fitting blocks from j
             c = c == 0u ? 1u : c;                                      // a big (or implausible) block alone
             gfb = t == ng ? j : gfb;

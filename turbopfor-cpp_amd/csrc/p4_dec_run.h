@@ -84,16 +84,22 @@ struct RunPlaneT
     uint32_t span;       // bytes to stage
     uint32_t avail;      // readable bytes from the chunk base (stream end)
 
+    // A block whose offsets do not lie inside the stream (o <= e <= in_bytes)
+    // loads nothing -- whatever the offset values, no descriptor is based
+    // outside the stream -- and is reported by the length check (len =
+    // 0xFFFFFFFF).  (Round 5: a caller passing a 2-entry offset array for
+    // 3,200 blocks made the decoder read garbage offsets and fault.)
     __device__ __forceinline__ void init(uint64_t in_base, uint64_t in_end, uint64_t o, uint64_t e, bool valid)
     {
-        const uint64_t ab = in_base + o;
+        const bool inb = valid && e >= o && e <= in_end - in_base;
+        const uint64_t ab = in_base + (inb ? o : 0ull);
         const uint64_t cb = ab & ~15ull;
-        span = valid ? static_cast<uint32_t>(min_u64(sub_sat(in_base + e, cb), SLOT - 64)) : 0u;
-        avail = valid ? static_cast<uint32_t>(min_u64(sub_sat(in_end, cb), SLOT)) : 0u;
-        const bool slow = valid && ((!ONE && span > 2048u) || span + 16u > avail);
+        span = inb ? static_cast<uint32_t>(min_u64(sub_sat(in_base + e, cb), SLOT - 64)) : 0u;
+        avail = inb ? static_cast<uint32_t>(min_u64(sub_sat(in_end, cb), SLOT)) : 0u;
+        const bool slow = inb && ((!ONE && span > 2048u) || span + 16u > avail);
         ctl = (slow ? 0u : span) | ((static_cast<uint32_t>(ab) & 15u) << kCtlShift) | (slow ? kCtlSlow : 0u)
             | (!ONE && !slow && span > 1024u ? kCtlTwo : 0u) | (ONE && !slow && span > 1024u ? kCtlBig : 0u);
-        len = (e >= o && e - o < 0x10000ull) ? static_cast<uint32_t>(e - o) : 0xFFFFFFFFu;
+        len = (inb && e - o < 0x10000ull) ? static_cast<uint32_t>(e - o) : 0xFFFFFFFFu;
         cblo = static_cast<uint32_t>(cb);
         cbhi = static_cast<uint32_t>(cb >> 32);
     }
