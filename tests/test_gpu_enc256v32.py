@@ -160,11 +160,11 @@ def test_full_size_c3_sample_vs_oracle():
 @pytest.mark.parametrize("mode", [0, 3, 4, 5])
 @pytest.mark.parametrize("nb", [1, 15, 16, 17, 31, 33, 1000, 20_000])
 def test_encoder_entries_vs_oracle(mode, nb):
-    """The 256v32 encoder through the batch entry (mode 0, the library's own
-    choice of path) and both paths forced through the measurement library
-    (tpfm_enc256v32): 3 = two-pass (plan, run scan, write), 4 = slot (plan +
-    build into per-run slots, run scan, compaction), 5 = slot without the
-    fused plan/build scans.  Byte-exact vs the
+    """The 256v32 encoder through the batch entry (mode 0: the library's
+    two-pass encoder) and through the measurement library (tpfm_enc256v32):
+    3 = two-pass (plan, run scan, write), 4 / 5 = the slot encoder (plan +
+    build into per-run slots, run scan, compaction; with / without the fused
+    scans), measured and not adopted but kept byte-exact for A/B runs.  Byte-exact vs the
     oracle, mixed widths and exception rates, ragged last runs (a run is 16
     blocks)."""
     blocks = mixed_blocks(nb, nb + mode)

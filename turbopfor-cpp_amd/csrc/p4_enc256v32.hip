@@ -8,39 +8,23 @@
 // measured against the two-pass encoder and rejected in round 2 (decoupled
 // look-back over LDS-held tiles, the MALL-chunked pipelined launch, the
 // persistent-grid form) were A/B'd from scripts/enc_variants.hip
-// until round 4 (git history).
+// until round 4 (git history); round 5's slot encoder (values read once, a
+// compaction pass) lost too and lives in the measurement library
+// (measure/enc_slot.h).
 #include "p4_enc256v32.h"
 
 namespace tpf
 {
 
-size_t enc256v32_workspace(uint64_t nblocks) { return enc256::slot_workspace(nblocks); }
+size_t enc256v32_workspace(uint64_t nblocks) { return enc256::twopass_workspace(nblocks); }
 
-static int enc_path()
-{
-    static const int p = [] {
-        const char * e = getenv("TPF_ENC_PATH");
-        return e ? atoi(e) : 0;
-    }();
-    return p;
-}
-
-// The path (round 5): the slot encoder (values read once,
-// p4_enc256v32.h) when the workspace holds the slots, else the two-pass
-// encoder.  TPF_ENC_PATH=1 / 2 / 3 forces two-pass / slot / slot without
-// the fused plan+build scans (A/B runs).
 hipError_t launch_enc256v32(const uint32_t * in, uint64_t nblocks, const uint32_t * starts, uint32_t start0, bool d1,
                             uint8_t * out, uint64_t out_cap, uint64_t * off, void * ws, size_t ws_bytes, hipStream_t stream)
 {
     if (nblocks == 0)
         return fill_u32(off, 0u, 2, stream);
-    if (nblocks + 1 > 0x7FFFFFFFull || ws_bytes < enc256::twopass_workspace(nblocks))
+    if (nblocks + 1 > 0x7FFFFFFFull || ws_bytes < enc256v32_workspace(nblocks))
         return hipErrorInvalidValue;
-    const bool slot_ok = ws_bytes >= enc256::slot_workspace(nblocks);
-    if (slot_ok && enc_path() == 2)
-        return enc256::launch_slot<true>(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream);
-    if (slot_ok && enc_path() == 3)
-        return enc256::launch_slot<false>(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream);
     return enc256::launch_twopass<0, 0>(in, nblocks, starts, start0, d1, out, out_cap, off, ws, stream);
 }
 

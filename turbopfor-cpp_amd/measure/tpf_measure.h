@@ -42,8 +42,10 @@ int tpfm_probe_hbm(int kind, void *d_dst, const void *d_src, uint64_t bytes, voi
  *            NOT a valid stream): each pass's data-movement ceiling;
  *   mode 3 = the two-pass encoder (plan, run scan, write);
  *   mode 4 = the slot encoder (plan + build into per-run slots, run scan,
- *            compaction); needs tpf_p4enc256v32_workspace_size bytes;
- *   mode 5 = the slot encoder without the fused plan/build scans. */
+ *            compaction: measured and not adopted, enc_slot.h);
+ *   mode 5 = the slot encoder without the fused plan/build scans.
+ * d_ws: tpfm_enc256v32_workspace_size(mode, nblocks) bytes. */
+size_t tpfm_enc256v32_workspace_size(int mode, uint64_t nblocks);
 int tpfm_enc256v32(int mode, const uint32_t *d_in, uint64_t nblocks, int d1, const uint32_t *d_starts, uint32_t start0,
                    uint8_t *d_out, uint64_t out_cap, uint64_t *d_off, void *d_ws, size_t ws_bytes, void *stream);
 

@@ -8,6 +8,7 @@
 #include "../csrc/p4_dec256v32.h"
 #include "../csrc/p4_dec256v64.h"
 #include "../csrc/p4_enc256v32.h"
+#include "enc_slot.h"
 #include "tpf_measure.h"
 
 namespace tpfm
@@ -71,6 +72,11 @@ int tpfm_probe_hbm(int kind, void * d_dst, const void * d_src, uint64_t bytes, v
     if (kind < 0 || kind > 2 || !d_dst || (kind != 1 && !d_src))
         return -1;
     return tpfm::rc(tpfm::launch_probe_hbm(kind, d_dst, d_src, bytes, static_cast<hipStream_t>(stream)));
+}
+
+size_t tpfm_enc256v32_workspace_size(int mode, uint64_t nblocks)
+{
+    return mode >= 4 ? tpf::enc256::slot_workspace(nblocks) : tpf::enc256::twopass_workspace(nblocks);
 }
 
 int tpfm_enc256v32(int mode, const uint32_t * d_in, uint64_t nblocks, int d1, const uint32_t * d_starts, uint32_t start0, uint8_t * d_out,

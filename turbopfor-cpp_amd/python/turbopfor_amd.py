@@ -181,6 +181,8 @@ def measure():
         M.tpfm_probe_hbm.argtypes = [ctypes.c_int, c_vp, c_vp, c_u64, c_vp]
         M.tpfm_enc256v32.argtypes = [ctypes.c_int, c_vp, c_u64, ctypes.c_int, c_vp, ctypes.c_uint32, c_vp, c_u64, c_vp, c_vp,
                                      ctypes.c_size_t, c_vp]
+        M.tpfm_enc256v32_workspace_size.argtypes = [ctypes.c_int, c_u64]
+        M.tpfm_enc256v32_workspace_size.restype = ctypes.c_size_t
         M.tpfm_run_scan_workspace_size.argtypes = [c_u64]
         M.tpfm_run_scan_workspace_size.restype = ctypes.c_size_t
         M.tpfm_run_scan.argtypes = [c_vp, c_u64, c_vp, c_vp, c_vp, ctypes.c_size_t, c_vp]
@@ -227,13 +229,14 @@ def probe_hbm(kind, dst, src, nbytes):
 def enc256v32_path(mode, values, out, d1=False, starts=None, start0=0):
     """The 256v32 encoder through a forced path (tpfm_enc256v32): mode 1 =
     plan pass as a wave OR, 2 = write pass copying values (plain only, not a
-    valid stream), 3 = the two-pass encoder, 4 = the slot encoder.  Returns
+    valid stream), 3 = the two-pass encoder (the library's), 4 / 5 = the slot
+    encoder with / without the fused scans (measured, not adopted).  Returns
     the offsets tensor [nblocks+1]."""
     import torch
 
     nb = values.numel() // 256
     offs = torch.empty(nb + 1, dtype=torch.int64, device=values.device)
-    ws_bytes = int(lib().tpf_p4enc256v32_workspace_size(nb))
+    ws_bytes = int(measure().tpfm_enc256v32_workspace_size(mode, nb))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=values.device)
     _mcheck(measure().tpfm_enc256v32(mode, _ptr(values), nb, 1 if d1 else 0, _ptr(starts), ctypes.c_uint32(start0 & 0xFFFFFFFF),
                                      _ptr(out), out.numel(), _ptr(offs), _ptr(ws), ws_bytes, _stream(torch)), "tpfm_enc256v32")
