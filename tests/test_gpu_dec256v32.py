@@ -176,7 +176,7 @@ def test_small_block_grouped_path_vs_oracle(pad, mix):
     out = tpf.dec256v32(packed, torch.from_numpy(bad).to(DEV), len(blocks), err=err)
     torch.cuda.synchronize()
     assert int(err.item()) == 776
-    assert_blocks_equal(as_u32(out)[:776 * 256], expect[:776], "grouped decode before the corruption")
+    assert_blocks_equal(as_u32(out)[:776], expect[:776], "grouped decode before the corruption")
 
 
 @pytest.mark.parametrize("small", [False, True])
@@ -200,4 +200,4 @@ def test_offsets_outside_the_stream_are_reported_not_followed(small):
         torch.cuda.synchronize()
         # block at-1 ends at the bad offset: it is the first one reported
         assert int(err.item()) == at - 1, (at, int(err.item()))
-        assert_blocks_equal(as_u32(out)[:(at - 1) * 256], expect[:at - 1], f"decode before offsets {at}")
+        assert_blocks_equal(as_u32(out)[:at - 1], expect[:at - 1], f"decode before offsets {at}")
