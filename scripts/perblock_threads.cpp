@@ -3,7 +3,8 @@
 // threads, src/dispatch.cpp:88-104) at T concurrent callers: each thread
 // encodes / decodes ITS OWN block K times with turbopfor::p4Enc256v32 /
 // p4Dec256v32, checking every returned end pointer and the decoded values.
-// One JSON line per T.
+// One JSON line per T.  PBT_MODE=2: request mailboxes in pinned host memory
+// (tpf_perblock_mode(2)) instead of device memory written through the BAR.
 // usage: perblock_threads K T1 [T2 ...]
 #include <atomic>
 #include <chrono>
@@ -15,6 +16,7 @@
 #include <vector>
 
 #include "turbopfor.h"
+#include "turbopfor_capi.h"
 
 static void fill_block(uint32_t * v, uint32_t seed)
 {
@@ -37,6 +39,12 @@ int main(int argc, char ** argv)
         return 2;
     }
     const int K = std::atoi(argv[1]);
+    const int mode = std::getenv("PBT_MODE") ? std::atoi(std::getenv("PBT_MODE")) : 0;
+    if (mode != 0 && tpf_perblock_mode(mode) < 0)
+    {
+        std::fprintf(stderr, "tpf_perblock_mode(%d) failed\n", mode);
+        return 2;
+    }
     for (int a = 2; a < argc; ++a)
     {
         const int T = std::atoi(argv[a]);
@@ -87,10 +95,10 @@ int main(int argc, char ** argv)
             (phase == 0 ? enc_s : dec_s) = wall;
         }
         const double calls = static_cast<double>(T) * K;
-        std::printf("{\"threads\": %d, \"calls_per_thread\": %d, \"dec_calls_per_s\": %.0f, \"dec_G_int32_per_s\": %.4f, "
+        std::printf("{\"mode\": %d, \"threads\": %d, \"calls_per_thread\": %d, \"dec_calls_per_s\": %.0f, \"dec_G_int32_per_s\": %.4f, "
                     "\"dec_us_per_call\": %.2f, \"enc_calls_per_s\": %.0f, \"enc_G_int32_per_s\": %.4f, \"enc_us_per_call\": %.2f, "
                     "\"bad\": %d}\n",
-                    T, K, calls / dec_s, calls * 256 / dec_s / 1e9, dec_s * T / calls * 1e6, calls / enc_s, calls * 256 / enc_s / 1e9,
+                    mode, T, K, calls / dec_s, calls * 256 / dec_s / 1e9, dec_s * T / calls * 1e6, calls / enc_s, calls * 256 / enc_s / 1e9,
                     enc_s * T / calls * 1e6, bad.load());
         std::fflush(stdout);
         if (bad.load())

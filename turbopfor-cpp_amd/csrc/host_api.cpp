@@ -23,12 +23,10 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
-#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
-#include <shared_mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -189,14 +187,20 @@ struct Server
     tpf::ServerCtl * ctl = nullptr; // device memory shared by the launch's workgroups
     std::atomic<tpf::ServerReq *> launched_rq{nullptr};
     std::mutex mu; // launches, event queries
-    // mailbox leases: a lock-free mask (64 mailboxes since round 5); callers
-    // wait on lease_cv only when every mailbox is taken
-    static_assert(tpf::kServerBoxes == 64, "one bit per mailbox");
-    std::atomic<uint64_t> free_mask{~0ull};
-    std::atomic<int> waiters{0};
-    std::mutex lease_mu;
-    std::condition_variable lease_cv;
-    std::atomic<uint32_t> reqno[tpf::kServerBoxes] = {};
+    // Mailbox leases (round 5): one lock word per mailbox, each on its own
+    // cache line, tried from a per-thread starting mailbox, so concurrent
+    // callers touch no shared line per call.  A pause (tpf::PerblockPause)
+    // takes every mailbox: the mailboxes are also the per-block calls' side
+    // of the pause.  (A shared free mask, a std::shared_mutex for the pause
+    // and packed request counters -- six contended read-modify-writes per
+    // call -- capped 8-64 callers at ~630k calls/s together.)
+    struct alignas(64) Box
+    {
+        std::atomic<uint32_t> busy{0};
+        std::atomic<uint32_t> reqno{0}; // last request number posted to this mailbox
+    };
+    Box box[tpf::kServerBoxes];
+    bool held = false; // every mailbox taken by the pause (pause thread only)
 
     static void * pinned(size_t bytes, void ** dev_view)
     {
@@ -285,7 +289,7 @@ struct Server
         stop_locked();
         for (uint32_t i = 0; i < tpf::kServerBoxes; ++i)
         {
-            const uint32_t r = reqno[i].load();
+            const uint32_t r = box[i].reqno.load();
             if (rq_dev)
                 __atomic_store_n(&rq_dev->box[i].req, r, __ATOMIC_RELAXED);
             __atomic_store_n(&rq_host->box[i].req, r, __ATOMIC_RELAXED);
@@ -294,8 +298,14 @@ struct Server
         std::atomic_thread_fence(std::memory_order_seq_cst);
     }
 
-    // A free mailbox, searched from a per-thread starting bit (threads
-    // spread over the mask instead of all racing for the lowest bit).
+    bool try_lease(uint32_t i)
+    {
+        uint32_t z = 0u;
+        return box[i].busy.load(std::memory_order_relaxed) == 0u &&
+               box[i].busy.compare_exchange_strong(z, 1u, std::memory_order_seq_cst);
+    }
+    // A free mailbox, searched from a per-thread starting mailbox (up to 64
+    // threads get distinct ones); past 64 concurrent callers, wait by yielding.
     int lease()
     {
         thread_local const uint32_t hint = [] {
@@ -304,28 +314,31 @@ struct Server
         }();
         for (;;)
         {
-            uint64_t m = free_mask.load(std::memory_order_relaxed);
-            while (m != 0u)
+            for (uint32_t k = 0; k < tpf::kServerBoxes; ++k)
             {
-                const uint64_t rot = (m >> hint) | (hint ? m << (64u - hint) : 0u); // bit j = mailbox (hint + j) % 64
-                const int i = static_cast<int>((hint + static_cast<uint32_t>(__builtin_ctzll(rot))) % tpf::kServerBoxes);
-                if (free_mask.compare_exchange_weak(m, m & ~(1ull << i), std::memory_order_acq_rel))
-                    return i;
+                const uint32_t i = (hint + k) % tpf::kServerBoxes;
+                if (try_lease(i))
+                    return static_cast<int>(i);
             }
-            std::unique_lock<std::mutex> g(lease_mu);
-            waiters.fetch_add(1);
-            lease_cv.wait(g, [&] { return free_mask.load() != 0u; });
-            waiters.fetch_sub(1);
+            std::this_thread::yield();
         }
     }
-    void release(int i)
+    void release(int i) { box[i].busy.store(0u, std::memory_order_release); }
+    // the pause side: every mailbox, as the calls holding them return
+    void hold_all()
     {
-        free_mask.fetch_or(1ull << i);
-        if (waiters.load() > 0)
-        {
-            std::lock_guard<std::mutex> g(lease_mu);
-            lease_cv.notify_one();
-        }
+        for (uint32_t i = 0; i < tpf::kServerBoxes; ++i)
+            while (!try_lease(i))
+                std::this_thread::yield();
+        held = true;
+    }
+    void release_all()
+    {
+        if (!held)
+            return; // created during the pause: its calls wait on the pending word
+        held = false;
+        for (uint32_t i = 0; i < tpf::kServerBoxes; ++i)
+            release(static_cast<int>(i));
     }
 
     // Make sure a launch serves `rq`.  Fast path: the running launch raised
@@ -344,7 +357,7 @@ struct Server
     {
         tpf::ServerReqBox * b = &rq->box[i];
         tpf::ServerAnsBox * a = &an->box[i];
-        const uint32_t r = reqno[i].fetch_add(1u) + 1u;
+        const uint32_t r = box[i].reqno.fetch_add(1u, std::memory_order_relaxed) + 1u;
         ensure(rq);
         _mm_sfence(); // the payload and fields (write-combined device memory) before the request word
         std::atomic_thread_fence(std::memory_order_release);
@@ -388,33 +401,22 @@ Server * g_srv[64] = {};
 
 // A resident server kernel keeps its stream busy, and HIP waits for every
 // stream of the device in hipFree / hipHostFree / hipDeviceSynchronize.  So
-// per-block server calls hold g_pause shared, and the library's own frees
-// (host_stream.cpp) hold it exclusively after stopping the servers
-// (tpf::PerblockPause): no server runs during a free and none can be
-// relaunched by another thread's call until the free has returned.
-// pthread rwlocks prefer readers: a thread issuing per-block calls back to
-// back would starve a pause forever, so a pending pause holds new calls back.
-std::shared_mutex g_pause;
-std::atomic<int> g_pause_waiting{0};
+// the library's own frees (host_stream.cpp) run inside a tpf::PerblockPause:
+// it raises g_pause_pending, takes every mailbox of every server (waiting for
+// the calls that hold them), stops the servers, and keeps the mailboxes until
+// it ends, so no server runs during the free and no call can relaunch one.
+// A call leases its mailbox and THEN reads g_pause_pending (both sequentially
+// consistent): either the pause sees the mailbox taken and waits for it, or
+// the call sees the pause and gives the mailbox back.  Pauses of different
+// threads take turns on g_pause_mu; a thread's nested pauses count depth.
+std::mutex g_pause_mu;
+std::atomic<int> g_pause_pending{0};
 
 // pauses this thread holds (tpf::PerblockPause nests; only depth 0 -> 1 locks)
 thread_local int t_pause_depth = 0;
 
-std::shared_lock<std::shared_mutex> perblock_enter()
-{
-    if (t_pause_depth > 0)
-        return std::shared_lock<std::shared_mutex>(); // this thread already excludes every other server user
-    while (g_pause_waiting.load(std::memory_order_acquire) > 0)
-        std::this_thread::yield();
-    return std::shared_lock<std::shared_mutex>(g_pause);
-}
-
-void pause_lock()
-{
-    g_pause_waiting.fetch_add(1, std::memory_order_acq_rel);
-    g_pause.lock();
-    g_pause_waiting.fetch_sub(1, std::memory_order_acq_rel);
-}
+void pause_lock();
+void pause_unlock();
 
 void stop_servers()
 {
@@ -453,13 +455,56 @@ Server & server()
     return *t_srv;
 }
 
+void pause_lock()
+{
+    g_pause_mu.lock();
+    g_pause_pending.fetch_add(1, std::memory_order_seq_cst);
+    std::lock_guard<std::mutex> g(g_srv_mu);
+    for (Server * s : g_srv)
+        if (s)
+            s->hold_all();
+}
+
+void pause_unlock()
+{
+    {
+        std::lock_guard<std::mutex> g(g_srv_mu);
+        for (Server * s : g_srv)
+            if (s)
+                s->release_all();
+    }
+    g_pause_pending.fetch_sub(1, std::memory_order_seq_cst);
+    g_pause_mu.unlock();
+}
+
+// A call's mailbox.  Inside a pause (the pausing thread holds every
+// mailbox) a call uses mailbox 0 without leasing it.
 struct BoxLease
 {
     Server & s;
     tpf::ServerReq * rq;
-    int i;
-    explicit BoxLease(Server & srv) : s(srv), rq(srv.current()), i(srv.lease()) { }
-    ~BoxLease() { s.release(i); }
+    int i = 0;
+    bool own = false;
+    explicit BoxLease(Server & srv) : s(srv), rq(nullptr)
+    {
+        if (t_pause_depth == 0)
+            for (;;)
+            {
+                while (g_pause_pending.load(std::memory_order_acquire) != 0)
+                    std::this_thread::yield();
+                i = s.lease();
+                if (g_pause_pending.load(std::memory_order_seq_cst) == 0)
+                    break;
+                s.release(i);
+            }
+        own = t_pause_depth == 0;
+        rq = s.current();
+    }
+    ~BoxLease()
+    {
+        if (own)
+            s.release(i);
+    }
     tpf::ServerReqBox * req() const { return &rq->box[i]; }
     tpf::ServerAnsBox * ans() const { return &s.an->box[i]; }
     void call() { s.call(rq, i); }
@@ -467,7 +512,6 @@ struct BoxLease
 
 unsigned char * enc_srv(int fmt, const void * in, unsigned n, unsigned char * out, bool d1, uint64_t start)
 {
-    const auto pause = perblock_enter();
     Server & S = server();
     BoxLease L(S);
     tpf::ServerReqBox * b = L.req();
@@ -496,7 +540,6 @@ const unsigned char * dec_srv(int fmt, const unsigned char * in, unsigned n, voi
     const uint64_t size = tpf_block_size(fmt, in, uint64_t(1) << 20, n, &written);
     if (size == 0 || size > tpf::kServerPayload)
         throw std::runtime_error("turbopfor_amd: malformed P4 block header");
-    const auto pause = perblock_enter();
     Server & S = server();
     BoxLease L(S);
     tpf::ServerReqBox * b = L.req();
@@ -604,7 +647,7 @@ PerblockPause::PerblockPause()
 PerblockPause::~PerblockPause()
 {
     if (--t_pause_depth == 0)
-        g_pause.unlock();
+        pause_unlock();
 }
 } // namespace tpf
 
@@ -742,6 +785,7 @@ int tpf_perblock_mode(int mode)
     if (mode < 0)
         return g_mode.load();
     const int m = mode == 1 || mode == 2 ? mode : 0;
+    const tpf::PerblockPause p; // no call in flight while the halves switch
     const int old = g_mode.exchange(m);
     if (old != m)
     {

@@ -180,6 +180,7 @@ __device__ __forceinline__ void write_run(const EncRun & R, const uint32_t * in,
                                           uint32_t * val, uint64_t out_base, uint64_t cap_end, uint32_t t)
 {
     const uint32_t stv = D1 ? R.start_lane(in, starts, start0, t) : 0u;
+    RunCopy rc;
     R.template walk<kEncNCWrite>(t, [&](u32x4 v, uint32_t jj) {
         if constexpr (D1)
             v = delta_encode(v, rl32(stv, jj), t);
@@ -198,12 +199,15 @@ __device__ __forceinline__ void write_run(const EncRun & R, const uint32_t * in,
         }
         const uint32_t sb = emit_block256<true>(img, val, P, v, t);
         wave_lds_sync();
-        copy_out_image16(img, sb, dst, size, cap_end, t);
+        // the run's blocks are contiguous: whole 16-byte chunks, the chunk a
+        // block ends in carried into the next block's image (RunCopy)
+        rc.put(img, sb, dst, size, jj + 1u == R.n, t);
         wave_lds_sync();
         // only [0, sb + size) can be non-zero: clear it for the next block
         zero_image(img, min((sb + size + 15u) >> 4, kImgU32 / 4u), t);
         wave_lds_sync();
     });
+    (void)cap_end; // the batch entry points require out_cap >= the bound: no chunk passes the stream's end
 }
 
 // ---- two-pass encoder (plan -> run scan -> write): the production path ---

@@ -10,7 +10,8 @@
 // one 16-byte load per lane per block, the layout of k_dec128v64w.
 // Each block is built in its own LDS image whose dword phase puts the base
 // payload on a dword (a 256v64 unit's second block starts at an arbitrary
-// byte), then copied out (copy_out_image16, p4_enc32.h).
+// byte), then copied out in whole 16-byte chunks, the chunk a block ends in
+// carried into the next block of the run (RunCopy, p4_enc32.h).
 #include "p4_scan.h"
 
 #include "p4_generic.h"
@@ -368,9 +369,10 @@ __global__ __launch_bounds__(256) void k_enc128v64_write(const uint64_t * __rest
     run_offsets(off, R.first, R.n, run_base(run_pre, run_tile, R.first / kEnc64Run), t, ov, ev);
     const uint64_t pwv = t < R.n ? plan[R.first + t] : 0ull;
     const uint64_t out_base = reinterpret_cast<uint64_t>(out);
-    const uint64_t cap_end = out_base + out_cap;
+    (void)out_cap; // tpf_enc_batch requires out_cap >= tpf_enc_bound: no chunk passes the stream's end
     zero_image(img, kImg64U32 / 4u, t);
     wave_lds_sync();
+    RunCopy rc; // the run's blocks are contiguous: whole 16-byte chunks (p4_enc32.h)
     R.walk(t, [&](const Chunk64 & c, uint32_t jj) {
         uint64_t x[2][2];
         unit_values<NB, D1>(c, D1 ? readlane_u64(stv, jj) : 0ull, t, x);
@@ -386,7 +388,7 @@ __global__ __launch_bounds__(256) void k_enc128v64_write(const uint64_t * __rest
             const uint64_t dst = out_base + o + (u == 0 ? 0u : size0);
             const uint32_t sb = emit_block128v64(img, val_all[wv], P, x[u][0], x[u][1], t);
             wave_lds_sync();
-            copy_out_image16(img, sb, dst, size, cap_end, t);
+            rc.put(img, sb, dst, size, u + 1u == NB && jj + 1u == R.n, t);
             wave_lds_sync();
             zero_image(img, min((sb + size + 15u) >> 4, kImg64U32 / 4u), t);
             wave_lds_sync();

@@ -358,16 +358,18 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
     wave_lds_sync();
     pack_base_runs<PAD>(img, pw, val, b, t);
     const uint32_t v0 = sb + 2u + 32u * b;
-    // Exception emission (round 4): the lane's i-th flagged value is taken
-    // from its flag mask (lowest set bit, cleared after use), its byte address
-    // is its rank (raw: 4 bytes each) or a wave scan of the vbyte lengths, and
-    // its bytes go out as plain LDS byte stores (every byte of the exception
-    // area has exactly one writer and the base payload ends before v0), no
-    // atomics.  A first round-4 form that let idle lanes OR zeros into the
-    // image was 27% slower on C3 (their atomics hit the dword of the lane next
-    // to them); byte stores under exec masks were level with the serial
-    // emission; the form below is 1.5% faster on C3.
-    // the most exceptions any lane holds (wave-uniform loop bound)
+    // Exception emission (round 5), in two steps so that the per-exception
+    // byte work runs once per 64 exceptions instead of once per exception a
+    // lane holds (the wave's maximum, 2-3 steps on C3's posting blocks):
+    //  1. rank scatter: the lane's i-th flagged value (lowest set bit of its
+    //     flag mask) goes to val[rank] -- `val` is free once pack_base_runs has
+    //     read it (a wave's LDS operations complete in order) -- and its
+    //     position byte straight to the block's last xn bytes;
+    //  2. lane r takes rank r: raw words at 4r, or vbytes at the exclusive
+    //     wave scan of the lengths (p4_scalar_internal.cpp:47-89, :163-197).
+    // Every lane stores in every step: bytes a lane does not own go to a
+    // trash area past the 256 ranks of `val`, so the steps carry no exec-mask
+    // sections and their SALU bookkeeping.
     const uint32_t mc = (__builtin_amdgcn_ballot_w64(cnt >= 1u) != 0u) + (__builtin_amdgcn_ballot_w64(cnt >= 2u) != 0u) +
                         (__builtin_amdgcn_ballot_w64(cnt >= 3u) != 0u) + (__builtin_amdgcn_ballot_w64(cnt >= 4u) != 0u);
     // ex[j] for a per-lane j as two levels of selects (a four-way ?: chain
@@ -376,56 +378,12 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
         const uint32_t e01 = (j & 1u) ? ex[1] : ex[0], e23 = (j & 1u) ? ex[3] : ex[2];
         return (j & 2u) ? e23 : e01;
     };
-    uint32_t rem = my;
-    // Every lane stores in every step: bytes a lane does not own that step
-    // (no i-th exception, or past the value's length) go to the lane's own
-    // dword of the staging area `val`, free once pack_base_runs has read it,
-    // so the steps carry no exec-mask sections and their SALU bookkeeping.
-    uint8_t * const trash = reinterpret_cast<uint8_t *>(val + t);
-    const uint32_t trash_at = static_cast<uint32_t>(trash - ib); // (mod 2^32: LDS addresses are 32-bit)
-    auto put = [&](bool own, uint32_t at, uint32_t k, uint32_t byte) {
-        ib[__builtin_unpredictable(own) ? at : trash_at + k] = static_cast<uint8_t>(byte);
+    const uint32_t trash_at = static_cast<uint32_t>(reinterpret_cast<uint8_t *>(val + 256u + (t & 15u)) - ib); // (mod 2^32: LDS addresses are 32-bit)
+    auto put = [&](bool own, uint32_t at, uint32_t byte) {
+        ib[__builtin_unpredictable(own) ? at : trash_at] = static_cast<uint8_t>(byte);
     };
-    if (P.raw)
-    {
-        // 0xFF, xn raw LE words, xn position bytes (p4_scalar_internal.cpp:163-197)
-        if (t == 0)
-            ib[v0] = 0xFFu;
-        const uint32_t pbase = v0 + 1u + 4u * P.xn;
-#pragma unroll
-        for (uint32_t i = 0; i < 4u; ++i)
-            if (i < mc)
-            {
-                const bool on = rem != 0u;
-                const uint32_t j = on ? static_cast<uint32_t>(__builtin_ctz(rem)) : 0u;
-                rem &= rem - 1u;
-                const uint32_t k = before + i, A = v0 + 1u + 4u * k, x = pick(j);
-                put(on, A, 0u, x);
-                put(on, A + 1u, 1u, x >> 8);
-                put(on, A + 2u, 2u, x >> 16);
-                put(on, A + 3u, 3u, x >> 24);
-                put(on, pbase + k, 0u, 4u * t + j);
-            }
-        return sb;
-    }
-    // vbPut32 (p4_scalar_internal.cpp:47-89): byte offsets from a wave scan of the lengths
-    uint32_t A, vtotal;
-    if constexpr (FUSE)
-    {
-        A = v0 + pre->lbefore;
-        vtotal = pre->vtotal;
-    }
-    else
-    {
-        uint32_t mylen = 0u;
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j)
-            mylen += vblen32(ex[j]) & (0u - ((my >> j) & 1u));
-        const uint32_t lincl = wave_incl_scan(mylen);
-        vtotal = __builtin_amdgcn_readlane(lincl, 63);
-        A = v0 + lincl - mylen;
-    }
-    const uint32_t pbase = v0 + vtotal;
+    const uint32_t pbase = sb + P.size - P.xn; // the position bytes end the block
+    uint32_t rem = my;
 #pragma unroll
     for (uint32_t i = 0; i < 4u; ++i)
         if (i < mc)
@@ -433,27 +391,55 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
             const bool on = rem != 0u;
             const uint32_t j = on ? static_cast<uint32_t>(__builtin_ctz(rem)) : 0u;
             rem &= rem - 1u;
-            const uint32_t x = pick(j);
-            const uint32_t d2 = x - 156u, d3 = x - 16540u;
-            const bool g1 = x >= 156u, g2 = x >= 16540u, g3 = x >= 2113692u, g4 = x > 0xFFFFFFu;
-            const uint32_t L = 1u + g1 + g2 + g3 + g4;
-            // the value's first four bytes (the fifth, of a 5-byte value, is
-            // x >> 24), selected by the range tests (an L == k chain compiled
-            // into exec-mask branches)
-            const uint32_t c2 = (0x9Cu + (d2 >> 8)) | ((d2 & 0xFFu) << 8);
-            const uint32_t c3 = (0xDCu + (d3 >> 16)) | ((d3 & 0xFFFFu) << 8);
-            const uint32_t c45 = (g4 ? 0xFDu : 0xFCu) | (x << 8);
-            const uint32_t c23 = __builtin_unpredictable(g2) ? c3 : c2;
-            const uint32_t c25 = __builtin_unpredictable(g3) ? c45 : c23;
-            const uint32_t lo = __builtin_unpredictable(g1) ? c25 : x;
-            put(on, A, 0u, lo);
-            put(on && L > 1u, A + 1u, 1u, lo >> 8);
-            put(on && L > 2u, A + 2u, 2u, lo >> 16);
-            put(on && L > 3u, A + 3u, 3u, lo >> 24);
-            put(on && L > 4u, A + 4u, 0u, x >> 24);
-            put(on, pbase + before + i, 1u, 4u * t + j);
-            A += on ? L : 0u;
+            const uint32_t k = before + i;
+            val[__builtin_unpredictable(on) ? k : 256u + (t & 15u)] = pick(j);
+            put(on, pbase + k, 4u * t + j);
         }
+    wave_lds_sync();
+    if (P.raw)
+    {
+        // 0xFF, xn raw LE words, the positions
+        if (t == 0)
+            ib[v0] = 0xFFu;
+        for (uint32_t c = 0; c < P.xn; c += 64u)
+        {
+            const uint32_t r = c + t;
+            const bool on = r < P.xn;
+            const uint32_t x = val[min(r, 255u)], A = v0 + 1u + 4u * r;
+            put(on, A, x);
+            put(on, A + 1u, x >> 8);
+            put(on, A + 2u, x >> 16);
+            put(on, A + 3u, x >> 24);
+        }
+        return sb;
+    }
+    uint32_t vb = v0; // byte of the chunk's first vbyte
+    for (uint32_t c = 0; c < P.xn; c += 64u)
+    {
+        const uint32_t r = c + t;
+        const bool on = r < P.xn;
+        const uint32_t x = val[min(r, 255u)];
+        const uint32_t d2 = x - 156u, d3 = x - 16540u;
+        const bool g1 = x >= 156u, g2 = x >= 16540u, g3 = x >= 2113692u, g4 = x > 0xFFFFFFu;
+        const uint32_t L = on ? 1u + g1 + g2 + g3 + g4 : 0u;
+        const uint32_t incl = wave_incl_scan(L);
+        const uint32_t A = vb + incl - L;
+        vb += __builtin_amdgcn_readlane(incl, 63);
+        // the value's first four bytes (the fifth, of a 5-byte value, is
+        // x >> 24), selected by the range tests (an L == k chain compiled
+        // into exec-mask branches)
+        const uint32_t c2 = (0x9Cu + (d2 >> 8)) | ((d2 & 0xFFu) << 8);
+        const uint32_t c3 = (0xDCu + (d3 >> 16)) | ((d3 & 0xFFFFu) << 8);
+        const uint32_t c45 = (g4 ? 0xFDu : 0xFCu) | (x << 8);
+        const uint32_t c23 = __builtin_unpredictable(g2) ? c3 : c2;
+        const uint32_t c25 = __builtin_unpredictable(g3) ? c45 : c23;
+        const uint32_t lo = __builtin_unpredictable(g1) ? c25 : x;
+        put(on, A, lo);
+        put(L > 1u, A + 1u, lo >> 8);
+        put(L > 2u, A + 2u, lo >> 16);
+        put(L > 3u, A + 3u, lo >> 24);
+        put(L > 4u, A + 4u, x >> 24);
+    }
     return sb;
 }
 
@@ -515,5 +501,69 @@ __device__ __forceinline__ void copy_out_image16(const uint32_t * img, uint32_t 
     }
 }
 
+
+// Copy-out of a wave's RUN of consecutive blocks (round 5): the blocks of a
+// run are contiguous in the output, so the 16-byte output chunk a block ends
+// in is completed by the next block of the same wave.  The wave carries the
+// chunk's bytes produced so far (lane t < 16 holds byte t) and places them in
+// the next block's image just before its first byte, so every chunk is
+// stored whole with one 16-byte store -- the per-block byte-store edges of
+// copy_out_image16 (head and tail chunks written by 32 lanes byte by byte,
+// every block) disappear.  Only the run's first chunk (its first `lead`
+// bytes belong to the previous run's wave) and its last chunk are partial,
+// written with byte stores.  Needs out_cap >= the stream's size (the batch
+// entry points check the bound), sb >= 16 (kImgLead) and a zeroed image in
+// front of the block.
+struct RunCopy
+{
+    uint32_t carry = 0u; // lane t < (next dst & 15): byte t of the open output chunk
+    uint32_t lead = 0u;  // bytes at the start of the open chunk that are not this run's
+    bool fresh = true;   // no block copied yet
+
+    // Block of `size` bytes at image byte sb, destined for dst; last: the
+    // run's last block (flush the open chunk).
+    __device__ __forceinline__ void put(uint32_t * img, uint32_t sb, uint64_t dst, uint32_t size, bool last, uint32_t t)
+    {
+        typedef __attribute__((address_space(1))) uint8_t gu8;
+        typedef __attribute__((address_space(1))) u32x4 gu32x4;
+        uint8_t * ib = reinterpret_cast<uint8_t *>(img);
+        const uint32_t ph = static_cast<uint32_t>(dst & 15u); // bytes of the open chunk already produced
+        if (fresh)
+        {
+            lead = ph;
+            fresh = false;
+        }
+        const uint32_t base = sb - ph; // image byte of the open chunk's byte 0
+        // the carried bytes in front of the block (lanes t < lead carry zeros: not stored)
+        if (t < ph)
+            ib[base + t] = static_cast<uint8_t>(carry);
+        wave_lds_sync();
+        gu8 * const a16 = (gu8 *)(dst & ~15ull);
+        const uint32_t end = ph + size;
+        const uint32_t nfull = end >> 4; // chunks completed by this block
+        const uint32_t k0 = lead != 0u ? 1u : 0u;
+        const uint32_t bs = base & 3u;
+        for (uint32_t k = k0 + t; k < nfull; k += 64u)
+        {
+            const uint32_t q = (base >> 2) + 4u * k;
+            const uint32_t w0 = img[q], w1 = img[q + 1], w2 = img[q + 2], w3 = img[q + 3], w4 = img[q + 4];
+            const u32x4 c = u32x4{__builtin_amdgcn_alignbyte(w1, w0, bs), __builtin_amdgcn_alignbyte(w2, w1, bs),
+                                  __builtin_amdgcn_alignbyte(w3, w2, bs), __builtin_amdgcn_alignbyte(w4, w3, bs)};
+            *(gu32x4 *)(a16 + 16u * k) = c;
+        }
+        if (k0 != 0u && nfull != 0u)
+        {
+            // the run's first chunk: bytes [lead, 16) are ours
+            if (t >= lead && t < 16u)
+                a16[t] = ib[base + t];
+            lead = 0u;
+        }
+        const uint32_t r = end & 15u;
+        const uint32_t tb = base + 16u * nfull; // image byte of the new open chunk
+        carry = t < r ? static_cast<uint32_t>(ib[tb + t]) : 0u;
+        if (last && r != 0u && t >= lead && t < r)
+            a16[16u * nfull + t] = static_cast<uint8_t>(carry);
+    }
+};
 
 } // namespace tpf::dev
