@@ -5,6 +5,8 @@
 // p4Dec256v32, checking every returned end pointer and the decoded values.
 // One JSON line per T.  PBT_MODE=2: request mailboxes in pinned host memory
 // (tpf_perblock_mode(2)) instead of device memory written through the BAR.
+// PBT_N=n (< 256): p4Enc32 / p4Dec32 blocks of n values instead (a small
+// payload: separates the per-call round trip from moving the block).
 // usage: perblock_threads K T1 [T2 ...]
 #include <atomic>
 #include <chrono>
@@ -40,6 +42,13 @@ int main(int argc, char ** argv)
     }
     const int K = std::atoi(argv[1]);
     const int mode = std::getenv("PBT_MODE") ? std::atoi(std::getenv("PBT_MODE")) : 0;
+    const unsigned nv = std::getenv("PBT_N") ? static_cast<unsigned>(std::atoi(std::getenv("PBT_N"))) : 256u;
+    auto enc = [nv](uint32_t * v, unsigned char * o) {
+        return nv >= 256u ? turbopfor::p4Enc256v32(v, 256, o) : turbopfor::p4Enc32(v, nv, o);
+    };
+    auto dec = [nv](const unsigned char * i, uint32_t * o) {
+        return nv >= 256u ? turbopfor::p4Dec256v32(i, 256, o) : turbopfor::p4Dec32(i, nv, o);
+    };
     if (mode != 0 && tpf_perblock_mode(mode) < 0)
     {
         std::fprintf(stderr, "tpf_perblock_mode(%d) failed\n", mode);
@@ -61,7 +70,7 @@ int main(int argc, char ** argv)
                     uint32_t v[256], out[256];
                     unsigned char buf[4096];
                     fill_block(v, static_cast<uint32_t>(i));
-                    unsigned char * end = turbopfor::p4Enc256v32(v, 256, buf); // warm: also relaunches the server
+                    unsigned char * end = enc(v, buf); // warm: also relaunches the server
                     if (!end)
                     {
                         bad++;
@@ -75,14 +84,14 @@ int main(int argc, char ** argv)
                     {
                         if (phase == 0)
                         {
-                            if (turbopfor::p4Enc256v32(v, 256, buf) != end)
+                            if (enc(v, buf) != end)
                                 bad++;
                         }
-                        else if (turbopfor::p4Dec256v32(buf, 256, out) != end)
+                        else if (dec(buf, out) != end)
                             bad++;
                     }
                     secs[i] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-                    if (phase == 1 && std::memcmp(out, v, sizeof v) != 0)
+                    if (phase == 1 && std::memcmp(out, v, 4u * (nv >= 256u ? 256u : nv)) != 0)
                         bad++;
                 });
             while (ready.load() + bad.load() < T)
@@ -95,10 +104,10 @@ int main(int argc, char ** argv)
             (phase == 0 ? enc_s : dec_s) = wall;
         }
         const double calls = static_cast<double>(T) * K;
-        std::printf("{\"mode\": %d, \"threads\": %d, \"calls_per_thread\": %d, \"dec_calls_per_s\": %.0f, \"dec_G_int32_per_s\": %.4f, "
+        std::printf("{\"mode\": %d, \"n\": %u, \"threads\": %d, \"calls_per_thread\": %d, \"dec_calls_per_s\": %.0f, \"dec_G_int32_per_s\": %.4f, "
                     "\"dec_us_per_call\": %.2f, \"enc_calls_per_s\": %.0f, \"enc_G_int32_per_s\": %.4f, \"enc_us_per_call\": %.2f, "
                     "\"bad\": %d}\n",
-                    mode, T, K, calls / dec_s, calls * 256 / dec_s / 1e9, dec_s * T / calls * 1e6, calls / enc_s, calls * 256 / enc_s / 1e9,
+                    mode, nv, T, K, calls / dec_s, calls * (nv >= 256u ? 256u : nv) / dec_s / 1e9, dec_s * T / calls * 1e6, calls / enc_s, calls * (nv >= 256u ? 256u : nv) / enc_s / 1e9,
                     enc_s * T / calls * 1e6, bad.load());
         std::fflush(stdout);
         if (bad.load())

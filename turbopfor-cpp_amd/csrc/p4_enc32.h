@@ -67,24 +67,14 @@ template <bool FUSE = false>
 __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist, uint32_t t, VbPre * pre = nullptr)
 {
     Plan32 P;
-    const uint32_t orv = uni(wave_or(v.x | v.y | v.z | v.w));
-    if (orv == 0u)
-    {
-        P.b = 0;
-        P.bx = 0;
-        P.size = 1;
-        P.xn = 0;
-        P.raw = 0;
-        return P;
-    }
-    const uint32_t maxb = bw32(orv);
     const uint32_t first = __builtin_amdgcn_readlane(v.x, 0);
     // constant block: a ballot, not a wave reduction
     if (__builtin_amdgcn_ballot_w64(!((v.x == first) & (v.y == first) & (v.z == first) & (v.w == first))) == 0ull)
     {
-        P.b = maxb;
-        P.bx = 34;
-        P.size = 1u + ((maxb + 7u) >> 3);
+        const uint32_t cb = bw32(first);
+        P.b = cb;
+        P.bx = first == 0u ? 0u : 34u; // all zero: the plain b = 0 block
+        P.size = first == 0u ? 1u : 1u + ((cb + 7u) >> 3);
         P.xn = 0;
         P.raw = 0;
         return P;
@@ -100,6 +90,9 @@ __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist
     wave_lds_sync();
     const uint32_t cnt = PlanHist::get(hist, t == 0u ? 0u : (t <= 32u ? 33u - t : 64u)); // lane c: cnt[c] (0 for c > 32)
     wave_lds_sync();
+    // the block's bit width: the highest width with a count (a ballot and a
+    // scalar bit scan instead of a wave OR reduction of the values, round 5)
+    const uint32_t maxb = 63u - static_cast<uint32_t>(__builtin_clzll(__builtin_amdgcn_ballot_w64(cnt != 0u)));
     // suffix sums S(k) = #values with bw > k, then
     // vbsum(b) = S(b) + S(b+7) + 2 S(b+15) + 3 S(b+19) + 4 S(b+25): the shifted
     // sums come back through the histogram's LDS (one write, two ds_read2)
@@ -182,7 +175,15 @@ __device__ __forceinline__ Plan32 plan_block256(const u32x4 & v, uint32_t * hist
     const uint32_t xn = uni(count_ge(1u));
     P.xn = xn;
     P.bx = 33;
-    const uint32_t sumlen = uni(xn + count_ge(156u) + count_ge(16540u) + count_ge(2113692u) + count_ge(0x1000000u));
+    // y < 2^(maxb - b): the thresholds no y can reach are not counted (C3's
+    // posting blocks: y < 2^12, two of five counts; round 5)
+    const uint64_t ymax = (1ull << (maxb - b)) - 1ull;
+    uint32_t sumlen = xn + count_ge(156u);
+    if (ymax >= 16540u)
+        sumlen += count_ge(16540u);
+    if (ymax >= 2113692u)
+        sumlen += count_ge(2113692u) + (ymax >= 0x1000000u ? count_ge(0x1000000u) : 0u);
+    sumlen = uni(sumlen);
     P.raw = (sumlen + 32u > 4u * xn) ? 1u : 0u;
     const uint32_t vsize = P.raw ? 1u + 4u * xn : sumlen;
     P.size = 2u + 32u * b + vsize + xn;
@@ -218,7 +219,11 @@ __device__ __forceinline__ void or_bits(uint32_t * img, uint32_t bp, uint32_t va
 // 8l + r reads element 32r + l + 8j, ds_read_b32 banks (a/4) % 32 per 32-lane
 // half) land on 32 distinct banks instead of 8-way on 4 (A/B, C4 encode:
 // 455-458 -> 460-464 G int32/s)
-constexpr uint32_t kEncValU32 = 256 + 32;
+// + 64 trash dwords, one per lane, past the PAD layout (which ends at 284):
+// bytes a lane does not own in the exception steps go to ITS OWN dword (a
+// trash dword shared by lanes serialises their stores)
+constexpr uint32_t kEncValU32 = 256 + 32 + 64;
+constexpr uint32_t kEncTrash = 256 + 32;
 template <bool PAD>
 __device__ __forceinline__ uint32_t val_idx(uint32_t e)
 {
@@ -362,14 +367,21 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
     // byte work runs once per 64 exceptions instead of once per exception a
     // lane holds (the wave's maximum, 2-3 steps on C3's posting blocks):
     //  1. rank scatter: the lane's i-th flagged value (lowest set bit of its
-    //     flag mask) goes to val[rank] -- `val` is free once pack_base_runs has
-    //     read it (a wave's LDS operations complete in order) -- and its
+    //     flag mask) goes to val[rank] -- `val` is free once pack_base_runs
+    //     has read it (a wave's LDS operations complete in order) -- and its
     //     position byte straight to the block's last xn bytes;
     //  2. lane r takes rank r: raw words at 4r, or vbytes at the exclusive
     //     wave scan of the lengths (p4_scalar_internal.cpp:47-89, :163-197).
-    // Every lane stores in every step: bytes a lane does not own go to a
-    // trash area past the 256 ranks of `val`, so the steps carry no exec-mask
-    // sections and their SALU bookkeeping.
+    // Every lane stores in every step: what a lane does not own goes to its
+    // own trash dword past the PAD layout, so the steps carry no exec-mask
+    // sections (measured: element-order values with the positions OR-ed in
+    // by every lane were 24% slower on C3 -- idle lanes' atomics on their
+    // neighbours' dwords serialise).
+    uint32_t * const trash = val + kEncTrash + t;
+    const uint32_t trash_at = static_cast<uint32_t>(reinterpret_cast<uint8_t *>(trash) - ib); // (mod 2^32: LDS addresses are 32-bit)
+    auto put = [&](bool own, uint32_t at, uint32_t byte) {
+        ib[__builtin_unpredictable(own) ? at : trash_at] = static_cast<uint8_t>(byte);
+    };
     const uint32_t mc = (__builtin_amdgcn_ballot_w64(cnt >= 1u) != 0u) + (__builtin_amdgcn_ballot_w64(cnt >= 2u) != 0u) +
                         (__builtin_amdgcn_ballot_w64(cnt >= 3u) != 0u) + (__builtin_amdgcn_ballot_w64(cnt >= 4u) != 0u);
     // ex[j] for a per-lane j as two levels of selects (a four-way ?: chain
@@ -377,10 +389,6 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
     auto pick = [&](uint32_t j) {
         const uint32_t e01 = (j & 1u) ? ex[1] : ex[0], e23 = (j & 1u) ? ex[3] : ex[2];
         return (j & 2u) ? e23 : e01;
-    };
-    const uint32_t trash_at = static_cast<uint32_t>(reinterpret_cast<uint8_t *>(val + 256u + (t & 15u)) - ib); // (mod 2^32: LDS addresses are 32-bit)
-    auto put = [&](bool own, uint32_t at, uint32_t byte) {
-        ib[__builtin_unpredictable(own) ? at : trash_at] = static_cast<uint8_t>(byte);
     };
     const uint32_t pbase = sb + P.size - P.xn; // the position bytes end the block
     uint32_t rem = my;
@@ -392,10 +400,11 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
             const uint32_t j = on ? static_cast<uint32_t>(__builtin_ctz(rem)) : 0u;
             rem &= rem - 1u;
             const uint32_t k = before + i;
-            val[__builtin_unpredictable(on) ? k : 256u + (t & 15u)] = pick(j);
+            *(__builtin_unpredictable(on) ? val + k : trash) = pick(j);
             put(on, pbase + k, 4u * t + j);
         }
     wave_lds_sync();
+    auto rank_value = [&](uint32_t r) { return val[min(r, 255u)]; };
     if (P.raw)
     {
         // 0xFF, xn raw LE words, the positions
@@ -405,7 +414,7 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
         {
             const uint32_t r = c + t;
             const bool on = r < P.xn;
-            const uint32_t x = val[min(r, 255u)], A = v0 + 1u + 4u * r;
+            const uint32_t x = rank_value(r), A = v0 + 1u + 4u * r;
             put(on, A, x);
             put(on, A + 1u, x >> 8);
             put(on, A + 2u, x >> 16);
@@ -418,9 +427,24 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
     {
         const uint32_t r = c + t;
         const bool on = r < P.xn;
-        const uint32_t x = val[min(r, 255u)];
-        const uint32_t d2 = x - 156u, d3 = x - 16540u;
-        const bool g1 = x >= 156u, g2 = x >= 16540u, g3 = x >= 2113692u, g4 = x > 0xFFFFFFu;
+        const uint32_t x = rank_value(r);
+        const uint32_t d2 = x - 156u;
+        const bool g1 = x >= 156u;
+        if (__builtin_amdgcn_ballot_w64(on && x >= 16540u) == 0ull)
+        {
+            // every value of the chunk takes 1 or 2 bytes (posting-list
+            // gaps: C3's blocks): no 3-5 byte forms (wave-uniform branch)
+            const uint32_t L = on ? 1u + g1 : 0u;
+            const uint32_t incl = wave_incl_scan(L);
+            const uint32_t A = vb + incl - L;
+            vb += __builtin_amdgcn_readlane(incl, 63);
+            const uint32_t lo = __builtin_unpredictable(g1) ? (0x9Cu + (d2 >> 8)) | ((d2 & 0xFFu) << 8) : x;
+            put(on, A, lo);
+            put(L > 1u, A + 1u, lo >> 8);
+            continue;
+        }
+        const uint32_t d3 = x - 16540u;
+        const bool g2 = x >= 16540u, g3 = x >= 2113692u, g4 = x > 0xFFFFFFu;
         const uint32_t L = on ? 1u + g1 + g2 + g3 + g4 : 0u;
         const uint32_t incl = wave_incl_scan(L);
         const uint32_t A = vb + incl - L;

@@ -444,45 +444,24 @@ __device__ __forceinline__ PlanG plan_block_g(const typename FmtTraits<F>::T v[4
     constexpr bool wide = Tr::wide;
     const uint32_t NE = Tr::N ? Tr::N : n;
     PlanG P{0, 0, 1, 0, 0};
-    uint32_t maxb;
-    uint64_t first;
-    if constexpr (wide)
-    {
-        uint64_t o = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j)
-            if (t + 64u * j < n)
-                o |= v[j];
-        const uint64_t orv = wave_or64(o);
-        maxb = bw64d(orv);
-        first = readlane64(static_cast<uint64_t>(v[0]), 0);
-    }
-    else
-    {
-        // 32-bit values: one wave OR and one readlane
-        uint32_t o = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j)
-            if (t + 64u * j < n)
-                o |= static_cast<uint32_t>(v[j]);
-        maxb = bw32(uni(wave_or(o)));
-        first = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(v[0])), 0));
-    }
-    if (maxb == 0u)
-    {
-        P.size = 1u + base_bytes<F>(NE, 0);
-        return P;
-    }
-    // constant block: a ballot, not a wave reduction
+    const uint64_t first = wide ? readlane64(static_cast<uint64_t>(v[0]), 0)
+                                : static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(v[0])), 0));
+    // constant block (all zero: the plain b = 0 block): a ballot, not a wave reduction
     bool same = true;
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j)
         same = same && (t + 64u * j >= n || static_cast<uint64_t>(v[j]) == first);
     if (__builtin_amdgcn_ballot_w64(!same) == 0ull)
     {
-        P.b = maxb;
+        if (first == 0ull)
+        {
+            P.size = 1u + base_bytes<F>(NE, 0);
+            return P;
+        }
+        const uint32_t cb = wide ? bw64d(first) : bw32(static_cast<uint32_t>(first));
+        P.b = cb;
         P.bx = W + 2u;
-        P.size = 1u + ((maxb + 7u) >> 3);
+        P.size = 1u + ((cb + 7u) >> 3);
         return P;
     }
     PlanGHist::zero(hist, t);
@@ -510,6 +489,10 @@ __device__ __forceinline__ PlanG plan_block_g(const typename FmtTraits<F>::T v[4
         cnt64 = uni(PlanGHist::get(hist, 64));
     }
     wave_lds_sync();
+    // the block's bit width: the highest width with a count (lane c holds
+    // cnt[c]; a ballot and a scalar bit scan instead of a wave OR reduction
+    // of the values, round 5); not all zero, so some width >= 1 has a count
+    const uint32_t maxb = cnt64 != 0u ? 64u : 63u - static_cast<uint32_t>(__builtin_clzll(__builtin_amdgcn_ballot_w64(cnt != 0u)));
     uint32_t ec, vbsum;
     if constexpr (!wide)
     {

@@ -28,7 +28,7 @@ namespace tpf::dev
 
 constexpr uint32_t kSrvImgU32 = (kServerPayload + 64u) / 4u;
 
-struct SrvLds
+struct alignas(16) SrvLds
 {
     uint32_t img[kSrvImgU32]; // staged block bytes (decode) / block image (encode)
     uint64_t scr[512];        // vbyte exception scratch of decode_block_g
@@ -46,6 +46,46 @@ __device__ __forceinline__ uint64_t ld_sys64(const uint64_t * p)
     return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Round 5: no system-scope fences.  On gfx950 an acquire fence at system
+// scope is `buffer_inv sc0 sc1` and a release `buffer_wbl2 sc0 sc1` --
+// whole-L2 invalidate / write-back operations of the XCD, which serialised
+// concurrent calls (64 mailboxes served ~0.7M calls/s together).  Instead
+// every access to the mailboxes' payloads is itself system-coherent (sc0 sc1:
+// it bypasses the CU and L2 caches), loads are issued only after the request
+// word they depend on has arrived, and the acknowledgement is stored only
+// after `s_waitcnt vmcnt(0)` has seen every payload store complete.
+constexpr int kSysPol = 1 | 16; // sc0 | sc1
+__device__ __forceinline__ void st_sys(uint32_t * p, uint32_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(uint64_t * p, uint64_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t ld_sys_v(const uint32_t * p)
+{
+    return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld_sys_v(const uint64_t * p)
+{
+    return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// bytes [0, nbytes) of an LDS buffer (16-byte aligned) to a mailbox answer
+// with 16-byte system-coherent stores: the answer crosses PCIe as 16-byte
+// writes instead of one write per dword (round 5).  Stores whole chunks (the
+// answer payload is larger than any result).
+__device__ __forceinline__ void put_answer(uint8_t * dst, const uint32_t * src, uint32_t nbytes, uint32_t t)
+{
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(dst, kServerPayload);
+    for (uint32_t i = t; i < (nbytes + 15u) >> 4; i += 64u)
+        __builtin_amdgcn_raw_buffer_store_b128(reinterpret_cast<const u32x4 *>(src)[i], rs, static_cast<int>(16u * i), 0, kSysPol);
+}
+
+// every vector memory operation of the wave complete (stores included: gfx9
+// counts them in vmcnt); "memory": the compiler keeps accesses on their side
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 __device__ __forceinline__ uint32_t rl32w(uint32_t v, uint32_t lane)
 {
     return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(lane)));
@@ -54,11 +94,12 @@ __device__ __forceinline__ uint32_t rl32w(uint32_t v, uint32_t lane)
 // Stage bytes [0, len) of a host buffer into LDS (and zero the 64 after).
 __device__ __forceinline__ void srv_stage(uint32_t * img, const uint8_t * src, uint32_t len, uint32_t t)
 {
-    const u32x4 * s = reinterpret_cast<const u32x4 *>(src);
+    // system-coherent 16-byte loads (kSysPol); chunks past len read nothing
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(src, kServerPayload);
     u32x4 * d = reinterpret_cast<u32x4 *>(img);
     const uint32_t n16 = (len + 15u) >> 4;
     for (uint32_t i = t; i < n16 + 4u && i < kSrvImgU32 / 4u; i += 64u)
-        d[i] = i < n16 ? s[i] : u32x4{0u, 0u, 0u, 0u};
+        d[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(i < n16 ? 16u * i : 0x80000000u), 0, kSysPol);
     wave_lds_sync();
     // bytes of the last chunk past len were read from the payload buffer: clear them
     uint8_t * b = reinterpret_cast<uint8_t *>(img);
@@ -69,11 +110,11 @@ __device__ __forceinline__ void srv_stage(uint32_t * img, const uint8_t * src, u
 
 // One F block at LDS byte s: values -> out (T), returns bytes consumed;
 // *lim = values the reference writes (n for a constant block, else the
-// layout's width).  D1: start -> *last (value n-1).
+// layout's width).  D1: start -> *last (value n-1).  The values go out
+// through L.scr (free once the block is decoded) as 16-byte stores.
 template <Fmt F>
 __device__ __forceinline__ uint32_t srv_dec_one(SrvLds & L, uint32_t s, uint32_t n, bool d1, typename FmtTraits<F>::T start,
-                                                typename FmtTraits<F>::T * out, uint32_t t, uint32_t * lim,
-                                                typename FmtTraits<F>::T * last)
+                                                uint8_t * out, uint32_t t, uint32_t * lim, typename FmtTraits<F>::T * last)
 {
     using T = typename FmtTraits<F>::T;
     const uint32_t NE = FmtTraits<F>::N ? FmtTraits<F>::N : n;
@@ -83,10 +124,13 @@ __device__ __forceinline__ uint32_t srv_dec_one(SrvLds & L, uint32_t s, uint32_t
     if (d1)
         *last = delta1_g<T>(v, n, start, t); // its carry: the value of element n-1
     *lim = cm ? n : NE;
+    wave_lds_sync(); // the decoder's scratch reads are done
+    T * const st = reinterpret_cast<T *>(L.scr);
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j)
-        if (t + 64u * j < *lim)
-            out[t + 64u * j] = v[j];
+        st[t + 64u * j] = v[j];
+    wave_lds_sync();
+    put_answer(out, reinterpret_cast<const uint32_t *>(L.scr), *lim * static_cast<uint32_t>(sizeof(T)), t);
     wave_lds_sync();
     return used;
 }
@@ -102,7 +146,7 @@ __device__ __forceinline__ uint32_t srv_enc_one(SrvLds & L, uint32_t s, const ty
     T v[4];
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j)
-        v[j] = t + 64u * j < NE ? in[t + 64u * j] : T(0);
+        v[j] = t + 64u * j < NE ? ld_sys_v(&in[t + 64u * j]) : T(0);
     if (d1)
         delta_enc_g<T>(v, start, n, t);
     const PlanG P = plan_block_g<F>(v, n, L.hist, t);
@@ -120,7 +164,7 @@ __device__ __forceinline__ void srv_serve(SrvLds & L, const ServerReqBox * box, 
     if (op == kOpDec)
     {
         srv_stage(L.img, box->in, in_len, t);
-        T * out = reinterpret_cast<T *>(ans->out);
+        uint8_t * const out = ans->out;
         uint32_t lim = 0;
         T last = T(0);
         uint32_t used = srv_dec_one<F>(L, 0u, n0, d1, static_cast<T>(start), out, t, &lim, &last);
@@ -135,14 +179,14 @@ __device__ __forceinline__ void srv_serve(SrvLds & L, const ServerReqBox * box, 
             if (ok)
             {
                 // second 128v64 block, starting after the first one's value 127
-                used += srv_dec_one<F>(L, used, n - 128u, d1, last, out + 128, t, &lim, &last);
+                used += srv_dec_one<F>(L, used, n - 128u, d1, last, out + 128u * sizeof(T), t, &lim, &last);
                 written = 128u + lim;
             }
         }
         if (t == 0)
         {
-            ans->result = ok && used == in_len ? used : 0xFFFFFFFFu;
-            ans->written = written;
+            st_sys(&ans->result, ok && used == in_len ? used : 0xFFFFFFFFu);
+            st_sys(&ans->written, written);
         }
         return;
     }
@@ -159,12 +203,10 @@ __device__ __forceinline__ void srv_serve(SrvLds & L, const ServerReqBox * box, 
         const T s127 = static_cast<T>(uni64(ld_sys64(reinterpret_cast<const uint64_t *>(in + 127))));
         size += srv_enc_one<F>(L, size, in + 128, n - 128u, d1, s127, t);
     }
-    // copy the image out (whole dwords: the mailbox payload is larger than any block)
-    uint32_t * dst = reinterpret_cast<uint32_t *>(ans->out);
-    for (uint32_t i = t; i < (size + 3u) >> 2; i += 64u)
-        dst[i] = L.img[i];
+    // copy the image out (whole 16-byte chunks: the mailbox payload is larger than any block)
+    put_answer(ans->out, L.img, size, t);
     if (t == 0)
-        ans->result = size;
+        st_sys(&ans->result, size);
 }
 
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t * p)
@@ -198,7 +240,8 @@ __global__ __launch_bounds__(256) void k_block_server(ServerReq * rq, ServerAns 
         const uint32_t r = rl32w(word, 0);
         if (r != last)
         {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // system scope: the payload
+            // (no acquire fence: the payload loads are system-coherent and
+            // issued after this request word arrived)
             const uint32_t op = rl32w(word, 1), fmt = rl32w(word, 2), n = rl32w(word, 3);
             const uint32_t d1 = rl32w(word, 4), in_len = rl32w(word, 5);
             const uint64_t start = (static_cast<uint64_t>(rl32w(word, 7)) << 32) | rl32w(word, 6);
@@ -206,7 +249,7 @@ __global__ __launch_bounds__(256) void k_block_server(ServerReq * rq, ServerAns 
             if (!ok)
             {
                 if (t == 0)
-                    ans->result = 0xFFFFFFFFu;
+                    st_sys(&ans->result, 0xFFFFFFFFu);
             }
             else
                 switch (fmt)
@@ -231,9 +274,9 @@ __global__ __launch_bounds__(256) void k_block_server(ServerReq * rq, ServerAns 
                         break;
                     default:
                         if (t == 0)
-                            ans->result = 0xFFFFFFFFu;
+                            st_sys(&ans->result, 0xFFFFFFFFu);
                 }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); // results before the acknowledgement
+            wait_vm(); // the results reached memory before the acknowledgement
             if (t == 0)
                 __hip_atomic_store(&ans->ack, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             last = r;
