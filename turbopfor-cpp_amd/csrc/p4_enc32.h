@@ -366,12 +366,14 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
     // Exception emission (round 5), in two steps so that the per-exception
     // byte work runs once per 64 exceptions instead of once per exception a
     // lane holds (the wave's maximum, 2-3 steps on C3's posting blocks):
-    //  1. rank scatter: the lane's i-th flagged value (lowest set bit of its
-    //     flag mask) goes to val[rank] -- `val` is free once pack_base_runs
-    //     has read it (a wave's LDS operations complete in order) -- and its
-    //     position byte straight to the block's last xn bytes;
-    //  2. lane r takes rank r: raw words at 4r, or vbytes at the exclusive
-    //     wave scan of the lengths (p4_scalar_internal.cpp:47-89, :163-197).
+    //  1. the shifted values go to val[4t + j] in element order (one 16-byte
+    //     store; `val` is free once pack_base_runs has read it, a wave's LDS
+    //     operations complete in order) and the lane's i-th flagged element
+    //     (lowest set bit of its flag mask) writes its position byte to rank
+    //     before + i of the block's last xn bytes;
+    //  2. lane r takes rank r: its position byte names its value; raw words
+    //     at 4r, or vbytes at the exclusive wave scan of the lengths
+    //     (p4_scalar_internal.cpp:47-89, :163-197).
     // Every lane stores in every step: what a lane does not own goes to its
     // own trash dword past the PAD layout, so the steps carry no exec-mask
     // sections (measured: element-order values with the positions OR-ed in
@@ -384,13 +386,8 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
     };
     const uint32_t mc = (__builtin_amdgcn_ballot_w64(cnt >= 1u) != 0u) + (__builtin_amdgcn_ballot_w64(cnt >= 2u) != 0u) +
                         (__builtin_amdgcn_ballot_w64(cnt >= 3u) != 0u) + (__builtin_amdgcn_ballot_w64(cnt >= 4u) != 0u);
-    // ex[j] for a per-lane j as two levels of selects (a four-way ?: chain
-    // was compiled into exec-mask branches)
-    auto pick = [&](uint32_t j) {
-        const uint32_t e01 = (j & 1u) ? ex[1] : ex[0], e23 = (j & 1u) ? ex[3] : ex[2];
-        return (j & 2u) ? e23 : e01;
-    };
     const uint32_t pbase = sb + P.size - P.xn; // the position bytes end the block
+    *reinterpret_cast<u32x4 *>(val + 4u * t) = u32x4{ex[0], ex[1], ex[2], ex[3]};
     uint32_t rem = my;
 #pragma unroll
     for (uint32_t i = 0; i < 4u; ++i)
@@ -399,12 +396,10 @@ __device__ __forceinline__ uint32_t emit_block256(uint32_t * img, uint32_t * val
             const bool on = rem != 0u;
             const uint32_t j = on ? static_cast<uint32_t>(__builtin_ctz(rem)) : 0u;
             rem &= rem - 1u;
-            const uint32_t k = before + i;
-            *(__builtin_unpredictable(on) ? val + k : trash) = pick(j);
-            put(on, pbase + k, 4u * t + j);
+            put(on, pbase + before + i, 4u * t + j);
         }
     wave_lds_sync();
-    auto rank_value = [&](uint32_t r) { return val[min(r, 255u)]; };
+    auto rank_value = [&](uint32_t r) { return val[ib[pbase + min(r, P.xn - 1u)]]; };
     if (P.raw)
     {
         // 0xFF, xn raw LE words, the positions
