@@ -506,12 +506,16 @@ __device__ __forceinline__ PlanG plan_block_g(const typename FmtTraits<F>::T v[4
     }
     else
     {
-        auto at = [&](uint32_t c) -> uint32_t {
-            // ds_bpermute takes lane c mod 64 from address bits [7:2]
-            const uint32_t x = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(c << 2), static_cast<int>(cnt)));
-            return c < 64u ? x : (c == 64u ? cnt64 : 0u);
-        };
-        const uint32_t vbacc = at(t + 7u) + 2u * at(t + 15u) + 3u * at(t + 19u) + 4u * at(t + 25u);
+        // cnt[c] for c = t+7, t+15, t+19, t+25 back through the histogram's
+        // LDS (cnt[64] = cnt64, zeros past it; the bins were read above):
+        // one store and four reads at immediate offsets instead of four
+        // ds_bpermute with their address and range selects (round 5)
+        hist[t] = cnt;
+        if (t < 25u)
+            hist[64u + t] = t == 0u ? cnt64 : 0u;
+        wave_lds_sync();
+        const uint32_t vbacc = hist[t + 7u] + 2u * hist[t + 15u] + 3u * hist[t + 19u] + 4u * hist[t + 25u];
+        wave_lds_sync();
         // both suffix sums in one scan (cnt <= 256 low half, cnt + vbacc <= 11*256 high half)
         const uint32_t pab = wave_incl_scan(cnt | ((cnt + vbacc) << 16));
         const uint32_t tab = __builtin_amdgcn_readlane(pab, 63);
