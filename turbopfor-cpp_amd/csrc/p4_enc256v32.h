@@ -72,7 +72,9 @@ __device__ __forceinline__ Plan32 unplan(uint32_t w, uint32_t size)
 // arrive through a buffer descriptor over exactly the run's n KB, so the
 // pipelined loads of blocks >= n return zeros without memory traffic and
 // every path has the same vmcnt pattern (see RunPlane, p4_dec_run.h).
-struct EncRun
+// POL: cache policy of the value loads (buffer-load aux bits)
+template <int POL = 0>
+struct EncRunT
 {
     uint64_t first;
     uint32_t n;
@@ -99,7 +101,7 @@ struct EncRun
 
     __device__ __forceinline__ u32x4 load(uint32_t jj, uint32_t t) const
     {
-        return __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(jj * 1024u + 16u * t), 0, 0);
+        return __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(jj * 1024u + 16u * t), 0, POL);
     }
 
     // Start value of block first+t for delta-1 (lanes t < n): the given
@@ -140,14 +142,18 @@ struct EncRun
     }
 };
 
+using EncRun = EncRunT<0>;
+constexpr int kEncPolPlan = 2;  // plan pass value loads: nontemporal (C3 D1 encode +1.6%, C4 level; the write pass loses with it, r5r)
+constexpr int kEncPolWrite = 0; // write pass value loads
+
 __device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t lane)
 {
     return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(lane)));
 }
 
 // Plan a run: lane j of (szv, pwv) = size and plan word of block R.first+j.
-template <bool D1, int PROBE = 0>
-__device__ __forceinline__ void plan_run(const EncRun & R, const uint32_t * in, const uint32_t * starts, uint32_t start0,
+template <bool D1, int PROBE = 0, class Run>
+__device__ __forceinline__ void plan_run(const Run & R, const uint32_t * in, const uint32_t * starts, uint32_t start0,
                                          uint32_t * hist, uint32_t t, uint32_t & szv, uint32_t & pwv)
 {
     const uint32_t stv = D1 ? R.start_lane(in, starts, start0, t) : 0u;
@@ -174,8 +180,8 @@ __device__ __forceinline__ void plan_run(const EncRun & R, const uint32_t * in, 
 
 // Write a run: lane j of (szv, pwv, olo/ohi) = size, plan word and byte
 // offset of block R.first+j.  img: the wave's zeroed LDS image (left zeroed).
-template <bool D1, int PROBE = 0>
-__device__ __forceinline__ void write_run(const EncRun & R, const uint32_t * in, const uint32_t * starts, uint32_t start0,
+template <bool D1, int PROBE = 0, class Run>
+__device__ __forceinline__ void write_run(const Run & R, const uint32_t * in, const uint32_t * starts, uint32_t start0,
                                           uint32_t szv, uint32_t pwv, uint32_t olo, uint32_t ohi, uint32_t * img,
                                           uint32_t * val, uint64_t out_base, uint64_t cap_end, uint32_t t)
 {
@@ -226,7 +232,7 @@ __global__ __launch_bounds__(256) void k_enc256v32_plan(const uint32_t * __restr
     const uint32_t wv = uni(threadIdx.x >> 6);
     for (uint64_t g = blockIdx.x;; g += gridDim.x)
     {
-        EncRun R;
+        EncRunT<kEncPolPlan> R;
         if (!R.init_at(in, nblocks, (g * 4u + wv) * kEncRun, kEncRun))
             return;
         uint32_t szv, pwv; // lane j: block first+j
@@ -257,7 +263,7 @@ __global__ __launch_bounds__(256) void k_enc256v32_write(const uint32_t * __rest
     const uint64_t out_base = reinterpret_cast<uint64_t>(out);
     for (uint64_t g = blockIdx.x;; g += gridDim.x)
     {
-        EncRun R;
+        EncRunT<kEncPolWrite> R;
         if (!R.init_at(in, nblocks, (g * 4u + wv) * kEncRun, kEncRun))
             return;
         // lane j: destination offset (64-bit), size and plan of block first+j

@@ -24,6 +24,7 @@ constexpr uint32_t kEnc64Run = 16;    // units per wave run
 constexpr uint32_t kEnc64NC = 3;      // units in flight per wave
 constexpr uint32_t kImg64U32 = 592;   // block image: 4..7 lead + block (<= 2150 B) + slack
 constexpr uint32_t kVal64U32 = 128;   // staged low halves (b <= 32 base packing)
+constexpr int kEnc64PolPlan = 2;      // plan pass value loads: nontemporal (+1.5-3%, r5s)
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
@@ -233,8 +234,9 @@ __device__ __forceinline__ uint32_t emit_block128v64(uint32_t * img, uint32_t * 
     return sb;
 }
 
-// A wave's run of up to kEnc64Run consecutive units (NB blocks of 128 u64).
-template <uint32_t NB>
+// A wave's run of up to kEnc64Run consecutive units (NB blocks of 128 u64);
+// POL: cache policy of the value loads (buffer-load aux bits).
+template <uint32_t NB, int POL = 0>
 struct EncRun64
 {
     uint64_t first;
@@ -253,9 +255,9 @@ struct EncRun64
 
     __device__ __forceinline__ void load(Chunk64 & c, uint32_t jj, uint32_t t) const
     {
-        c.a = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(jj * 1024u * NB + 16u * t), 0, 0);
+        c.a = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(jj * 1024u * NB + 16u * t), 0, POL);
         if constexpr (NB == 2)
-            c.b = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(jj * 2048u + 1024u + 16u * t), 0, 0);
+            c.b = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(jj * 2048u + 1024u + 16u * t), 0, POL);
     }
 
     // value preceding unit first+t (lanes t < n): the given starts, or for one
@@ -320,7 +322,7 @@ __global__ __launch_bounds__(256) void k_enc128v64_plan(const uint64_t * __restr
     __shared__ __attribute__((aligned(16))) uint32_t hist[4][kPlanGHistU32];
     const uint32_t t = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
-    EncRun64<NB> R;
+    EncRun64<NB, kEnc64PolPlan> R;
     if (!R.init(in, nunits, wv))
         return;
     const uint64_t stv = D1 ? R.start_lane(in, starts, start0, t) : 0ull;
