@@ -233,6 +233,14 @@ __global__ __launch_bounds__(256) void k_block_server(ServerReq * rq, ServerAns 
     ServerAnsBox * ans = &an->box[bi];
     uint32_t last = uni(ld_sys(&ans->ack));
     const uint32_t * line = &box->req;
+    // Round 5: the launch's shared words are touched rarely.  Each wave
+    // publishes its activity (atomicMax of last_active) at most once per
+    // 1 ms of serving, and idle waves read the shared words every 256th
+    // poll: one device-scope atomic on one address per request, from every
+    // server wave on every XCD, capped all callers together at ~1M
+    // calls/s; without it 16 callers reach ~3M (profiles/r5t_*).  The idle
+    // exit tolerates the staleness (10 ms idle against 1 ms publication).
+    uint64_t pub_a = born;
     for (uint32_t polls = 0;; ++polls)
     {
         // the whole request line in one read: lanes 0..7 hold its first 8 words
@@ -280,8 +288,13 @@ __global__ __launch_bounds__(256) void k_block_server(ServerReq * rq, ServerAns 
             if (t == 0)
                 __hip_atomic_store(&ans->ack, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             last = r;
-            if (t == 0)
-                atomicMax(&ctl->last_active, static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+            const uint64_t now_a = __builtin_amdgcn_s_memrealtime();
+            if (now_a - pub_a > 100000u) // 1 ms of the 100 MHz counter
+            {
+                if (t == 0)
+                    atomicMax(&ctl->last_active, static_cast<unsigned long long>(now_a));
+                pub_a = now_a;
+            }
             if (__builtin_amdgcn_s_memrealtime() - born > max_ticks) // busy past the lifetime: leave after this answer
             {
                 if (t == 0)
@@ -291,10 +304,11 @@ __global__ __launch_bounds__(256) void k_block_server(ServerReq * rq, ServerAns 
             continue;
         }
         // leave together: once one wave of the launch quits (idle or told to
-        // stop) every other follows; the shared words are read every 16th poll
-        // (the stop word every 64th: each read of it crosses PCIe in mode 2)
+        // stop) every other follows; the shared words are read every 256th
+        // poll (the stop word every 256th too: each read of it crosses PCIe
+        // in mode 2)
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
-        if ((polls & 15u) == 0u)
+        if ((polls & 255u) == 0u)
         {
             const uint64_t la = __hip_atomic_load(&ctl->last_active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (uni(ld_agent(&ctl->quit)) != 0u || ((polls & 63u) == 0u && uni(ld_sys(&rq->stop)) != 0u) ||
