@@ -329,6 +329,64 @@ def test_per_block_server_concurrent_threads(nthreads):
     assert not errors, errors
 
 
+def test_per_block_pause_and_mode_switch_during_calls():
+    """Round 5: a pause takes every mailbox, so tpf_perblock_quiesce and
+    tpf_perblock_mode may run while other threads are inside per-block calls
+    (each waits for the calls in flight; new calls wait for it).  8 caller
+    threads round-trip their blocks while a 9th switches the mailbox half
+    (mode 0 <-> 2) and quiesces the server over and over: every result stays
+    byte-exact and no call hangs."""
+    import threading
+
+    L = capi()
+    L.tpf_p4Enc256v32.restype = ctypes.c_void_p
+    L.tpf_p4Enc256v32.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]
+    L.tpf_p4Dec256v32.restype = ctypes.c_void_p
+    L.tpf_p4Dec256v32.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]
+    L.tpf_perblock_mode.restype = ctypes.c_int
+    L.tpf_perblock_mode.argtypes = [ctypes.c_int]
+    old = L.tpf_perblock_mode(-1)
+    errors = []
+    done = threading.Event()
+
+    def worker(k):
+        try:
+            for v in datagen.c2_blocks(60, 1 + (5 * k) % 32, 10, seed=100 + k):
+                v = np.ascontiguousarray(v)
+                buf = np.zeros(4096, np.uint8)
+                end = L.tpf_p4Enc256v32(v.ctypes.data, 256, buf.ctypes.data)
+                assert end is not None
+                assert bytes(buf[: end - buf.ctypes.data]) == oracle_lib.encode("256v32", v)
+                out = np.zeros(256, np.uint32)
+                assert L.tpf_p4Dec256v32(buf.ctypes.data, 256, out.ctypes.data) == end
+                assert np.array_equal(out, v)
+        except Exception as e:  # noqa: BLE001
+            errors.append((k, repr(e)))
+
+    def switcher():
+        try:
+            i = 0
+            while not done.is_set():
+                L.tpf_perblock_mode(2 if i % 2 == 0 else 0)
+                L.tpf_perblock_quiesce()
+                i += 1
+        except Exception as e:  # noqa: BLE001
+            errors.append(("switcher", repr(e)))
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    sw = threading.Thread(target=switcher)
+    sw.start()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    done.set()
+    sw.join(timeout=60)
+    L.tpf_perblock_mode(old)
+    assert not any(t.is_alive() for t in ts + [sw]), "a per-block call or the switcher hung"
+    assert not errors, errors
+
+
 def test_per_block_server_idle_exit_and_mode_switch():
     """The block server leaves after 10 ms without a request and the next call
     relaunches it; switching between the server layouts (device / host
