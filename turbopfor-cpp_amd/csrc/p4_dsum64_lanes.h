@@ -60,8 +60,8 @@ __device__ __forceinline__ uint64_t base_sum4_lanes(const uint32_t * w, uint32_t
 #pragma unroll
         for (uint32_t l = 0; l < 5u; ++l)
             d[l] = w[q + l];
-        uint64_t firsts = 0ull, hi = 0ull;
-        uint32_t lo = 0u;
+        // the 4 folded dwords summed in 64 bits (base_sum_lanes, round 5)
+        uint64_t firsts = 0ull, acc = 0ull;
 #pragma unroll
         for (uint32_t l = 0; l < 4u; ++l)
         {
@@ -71,9 +71,10 @@ __device__ __forceinline__ uint64_t base_sum4_lanes(const uint32_t * w, uint32_t
 #pragma unroll
             for (uint32_t lv = 0; lv < P; ++lv)
                 z = (z & PA[lv]) + ((z >> W[lv]) & PB[lv]);
-            lo += __builtin_amdgcn_ubfe(z, 0u, T);
-            hi += z >> T;
+            acc += z;
         }
+        uint32_t lo = __builtin_amdgcn_ubfe(static_cast<uint32_t>(acc), 0u, T);
+        const uint64_t hi = acc >> T;
 #pragma unroll
         for (uint32_t lv = (P < 1u ? P : 1u); lv < L; ++lv)
             lo = (lo & QA[lv]) + ((lo >> W[lv]) & QB[lv]);

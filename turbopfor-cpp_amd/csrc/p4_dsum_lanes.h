@@ -158,7 +158,11 @@ __device__ __forceinline__ uint32_t base_sum_lanes(const uint32_t * w, uint32_t 
 #pragma unroll
         for (uint32_t l = 0; l < 9u; ++l)
             d[l] = w[q + l];
-        uint32_t firsts = 0u, lo = 0u, hi = 0u;
+        // the 8 folded dwords summed in 64 bits (one add with carry each,
+        // round 5): slots below T cannot carry into T, so the low T bits
+        // are their sums and the bits from T up the cut top slots' sum
+        uint32_t firsts = 0u;
+        uint64_t acc = 0ull;
 #pragma unroll
         for (uint32_t l = 0; l < 8u; ++l)
         {
@@ -168,9 +172,10 @@ __device__ __forceinline__ uint32_t base_sum_lanes(const uint32_t * w, uint32_t 
 #pragma unroll
             for (uint32_t lv = 0; lv < P; ++lv)
                 z = (z & PA[lv]) + ((z >> W[lv]) & PB[lv]);
-            lo += __builtin_amdgcn_ubfe(z, 0u, T);
-            hi += z >> T;
+            acc += z;
         }
+        uint32_t lo = __builtin_amdgcn_ubfe(static_cast<uint32_t>(acc), 0u, T);
+        const uint32_t hi = static_cast<uint32_t>(acc >> T);
         // levels pre..L-1 of each lane: a lane narrower in pre than the
         // wave's P (e.g. b = 6 beside b = 2) still needs levels pre..P-1
         // here, so the loop starts at the smallest pre any b < 32 has (1);
