@@ -209,3 +209,47 @@ def mixed_blocks(nb, seed):
         return np.concatenate([datagen.c2_blocks(1, int(bw), int(rng.choice([0, 5, 10, 25])), seed=int(i))
                                for i, bw in enumerate(bws)])
     return np.concatenate([datagen.c2_blocks(nb // 32 + 1, bw, 10, seed=bw) for bw in range(1, 33)])[:nb]
+
+
+@pytest.mark.parametrize("d1", [False, True])
+@pytest.mark.parametrize("nb", [1, 7, 16, 31, 32, 33, 65, 257])
+def test_tiny_blocks_run_copy(d1, nb):
+    """Round 5's run copy-out (RunCopy: whole 16-byte chunks, the chunk a
+    block ends in carried into the next block of the wave's run) on runs of
+    1-5 byte blocks -- all-zero blocks (1 byte), constant blocks (2-5 bytes),
+    D1 lists with a constant step (constant deltas) -- mixed with ordinary
+    blocks, ragged run ends (runs are 16 blocks, 32 for D1): byte-exact vs
+    the oracle, and no byte past the stream is written."""
+    rng = np.random.default_rng(nb * 7 + d1)
+    kinds = rng.integers(0, 4, nb)
+    blocks = np.zeros((nb, 256), dtype=np.uint32)
+    for i, k in enumerate(kinds):
+        if k == 1:
+            blocks[i] = np.uint32(rng.integers(1, 1 << 31))  # constant block
+        elif k == 2:
+            blocks[i] = datagen.c2_blocks(1, int(rng.integers(1, 33)), 10, seed=i)[0]
+        elif k == 3:
+            blocks[i] = np.uint32(rng.integers(0, 256))
+    starts = None
+    if d1:
+        # D1 input: running sums of (delta + 1) so that each block's deltas are `blocks`
+        flat = np.cumsum(blocks.astype(np.uint64).reshape(-1) + 1) + np.uint64(12345)
+        vals = (flat & 0xFFFFFFFF).astype(np.uint32).reshape(nb, 256)
+        st = np.empty(nb, dtype=np.uint32)
+        st[0] = 12345
+        st[1:] = vals[:-1, -1]
+        starts = st
+    else:
+        vals = blocks
+    exp_packed, exp_off = oracle_lib.enc256v32_batch(vals, starts=starts)
+    cap = int(tpf.lib().tpf_p4enc256v32_bound(nb))
+    out = torch.full((cap,), 0xA5, dtype=torch.uint8, device=DEV)
+    if d1:
+        packed, offs = tpf.enc256v32(dev_u32(vals), d1=True, start0=12345, out=out)
+    else:
+        packed, offs = tpf.enc256v32(dev_u32(vals), out=out)
+    total = int(offs[-1].item())
+    got = out.cpu().numpy()
+    np.testing.assert_array_equal(offs.cpu().numpy().astype(np.uint64), exp_off)
+    np.testing.assert_array_equal(got[:total], exp_packed)
+    assert (got[total:] == 0xA5).all()
