@@ -22,6 +22,10 @@ extern "C" {
  * removed (k_dec256v32w<Probe>): block i's staged bytes are written to
  * d_out[256*i..] unchanged.  The data-movement ceiling bench.py compares the
  * decoder with. */
+// the plain 256v32 decode through a forced load path: grouped = 0 single-block
+// pipeline, 1 grouped 1 KB loads (the library picks one per launch)
+int tpfm_dec256v32_path(int grouped, const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks, uint32_t *d_out,
+                        void *stream);
 int tpfm_probe256v32(const uint8_t *d_in, uint64_t in_bytes, const uint64_t *d_off, uint64_t nblocks, uint32_t *d_out,
                      void *stream);
 

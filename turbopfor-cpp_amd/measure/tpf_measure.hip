@@ -54,6 +54,30 @@ int tpfm_probe256v32(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d
     return tpfm::rc(hipGetLastError());
 }
 
+// The plain 256v32 decode through a forced load path (VERDICT r4 #6 sweep):
+// grouped = 0 the single-block pipeline, 1 the grouped 1 KB loads -- the two
+// instantiations the library chooses between per launch (dec_grouped).
+int tpfm_dec256v32_path(int grouped, const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nblocks, uint32_t * d_out,
+                        void * stream)
+{
+    namespace dev = tpf::dev;
+    if (nblocks == 0)
+        return 0;
+    if (!d_in || !d_off || !d_out)
+        return -1;
+    const dev::DecArgs A{d_in, in_bytes, d_off, nblocks, d_out, nullptr, 0u, nullptr, nullptr};
+    constexpr uint32_t run = dev::kRunDefault;
+    const uint32_t grid = static_cast<uint32_t>((nblocks + 4ull * run - 1) / (4ull * run));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (grouped)
+        hipLaunchKernelGGL((dev::k_dec256v32w<dev::StartMode::None, run, dev::kDecPol, dev::kDecNC, dev::kDecMinW, true, 1024u>), dim3(grid),
+                           dim3(256), 0, s, A);
+    else
+        hipLaunchKernelGGL((dev::k_dec256v32w<dev::StartMode::None, run, dev::kDecPol, dev::kDecNC, dev::kDecMinW, true, 0u>), dim3(grid),
+                           dim3(256), 0, s, A);
+    return tpfm::rc(hipGetLastError());
+}
+
 int tpfm_probe256v64(const uint8_t * d_in, uint64_t in_bytes, const uint64_t * d_off, uint64_t nunits, uint64_t * d_out, void * stream)
 {
     namespace dev = tpf::dev;

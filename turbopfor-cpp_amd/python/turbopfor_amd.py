@@ -177,6 +177,7 @@ def measure():
             build()
         M = ctypes.CDLL(MEASURE_PATH)
         M.tpfm_probe256v32.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp]
+        M.tpfm_dec256v32_path.argtypes = [ctypes.c_int, c_vp, c_u64, c_vp, c_u64, c_vp, c_vp]
         M.tpfm_probe256v64.argtypes = [c_vp, c_u64, c_vp, c_u64, c_vp, c_vp]
         M.tpfm_probe_hbm.argtypes = [ctypes.c_int, c_vp, c_vp, c_u64, c_vp]
         M.tpfm_enc256v32.argtypes = [ctypes.c_int, c_vp, c_u64, ctypes.c_int, c_vp, ctypes.c_uint32, c_vp, c_u64, c_vp, c_vp,
@@ -214,6 +215,17 @@ def probe256v32(packed, offsets, nblocks, out):
 
     _mcheck(measure().tpfm_probe256v32(_ptr(packed), packed.numel(), _ptr(offsets), nblocks, _ptr(out), _stream(torch)),
             "tpfm_probe256v32")
+    return out
+
+
+def dec256v32_path(grouped, packed, offsets, nblocks, out):
+    """Measurement only: the plain 256v32 decode through a forced load path
+    (tpfm_dec256v32_path: grouped 0 = single-block pipeline, 1 = grouped 1 KB
+    loads; the library chooses per launch)."""
+    import torch
+
+    _mcheck(measure().tpfm_dec256v32_path(1 if grouped else 0, _ptr(packed), packed.numel(), _ptr(offsets), nblocks, _ptr(out),
+                                          _stream(torch)), "tpfm_dec256v32_path")
     return out
 
 
