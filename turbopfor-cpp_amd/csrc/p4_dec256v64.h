@@ -123,7 +123,12 @@ __device__ __forceinline__ uint32_t decode_block128v64(const uint32_t * lds, uin
 __device__ __forceinline__ uint64_t delta1_128v64(uint64_t & x0, uint64_t & x1, uint64_t start)
 {
     const uint64_t a0 = x0 + 1u, a1 = a0 + x1 + 1u;
-    const uint64_t incl = wave_incl_scan64(a1);
+    // every lane's pair total below 2^26 (posting lists: small gaps): the
+    // 64-lane inclusive scan stays below 2^32, so one 32-bit DPP scan does
+    // instead of the three of wave_incl_scan64 (wave-uniform test, round 5)
+    const uint64_t incl = __builtin_amdgcn_ballot_w64(a1 >= (1ull << 26)) == 0ull
+                              ? static_cast<uint64_t>(wave_incl_scan(static_cast<uint32_t>(a1)))
+                              : wave_incl_scan64(a1);
     const uint64_t base = start + incl - a1;
     x0 = base + a0;
     x1 = base + a1;
