@@ -100,6 +100,9 @@ __device__ __forceinline__ typename FmtTraits<F>::T base_elem(const uint32_t * l
 // vbyte value at byte position c (marker already known): 32-bit markers
 // (vbGet32Inline, p4_scalar_internal.h:589-625) or 64-bit markers
 // (vbGet64Inline, :638-670).  Returns the value, *len = bytes consumed.
+// 64-bit markers: the 1-3 byte forms by selects, only the long form behind a
+// branch (round 5: C3 64-bit lists +3.4%, per-unit starts +4%,
+// profiles/r5ai_vbyte64_ab.txt).
 template <bool Wide>
 __device__ __forceinline__ uint64_t vbyte_value(const uint32_t * lds, uint32_t c, uint32_t m)
 {
@@ -118,16 +121,17 @@ __device__ __forceinline__ uint64_t vbyte_value(const uint32_t * lds, uint32_t c
     }
     else
     {
-        if (m < 0x98u)
-            return m;
         const uint32_t d = lds_u32(lds, c + 1u);
-        if (m < 0xD8u)
-            return ((m - 0x98u) << 8) + (d & 0xFFu) + 152u;
-        if (m < 0xF8u)
-            return (d & 0xFFFFu) + ((m - 0xD8u) << 16) + 16536u;
-        const uint32_t nb = m - 0xF8u + 3u;
-        const uint64_t x = lds_u64(lds, c + 1u);
-        return nb >= 8u ? x : (x & ((1ull << (8u * nb)) - 1ull));
+        const uint32_t v2 = ((m - 0x98u) << 8) + (d & 0xFFu) + 152u;
+        const uint32_t v3 = (d & 0xFFFFu) + ((m - 0xD8u) << 16) + 16536u;
+        uint64_t r = m < 0x98u ? m : m < 0xD8u ? v2 : v3;
+        if (m >= 0xF8u)
+        {
+            const uint32_t nb = m - 0xF8u + 3u;
+            const uint64_t x = lds_u64(lds, c + 1u);
+            r = nb >= 8u ? x : (x & ((1ull << (8u * nb)) - 1ull));
+        }
+        return r;
     }
 }
 
