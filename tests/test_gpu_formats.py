@@ -204,3 +204,37 @@ def test_p4dec32_windows_oversize_block_reported():
     tpf.dec_batch("32", short, torch.from_numpy(off.astype(np.int64)).to(DEV), nb, n, err=err)
     torch.cuda.synchronize()
     assert int(err.item()) == 150
+
+
+def test_256v64_vbyte_every_marker_form():
+    """128v64 vbyte exceptions of every vbyte64 length form (1-3 byte markers
+    below 0xF8 and the 3..9-byte long forms, p4_scalar_internal.h:638-670):
+    few large exceptions over a 3-bit base make the encoder pick vbyte mode;
+    bytes against the oracle, values back from the batch decoder (plain and
+    D1 per-unit starts)."""
+    rng = np.random.default_rng(11)
+    nu = 512
+    blocks = rng.integers(0, 8, size=(nu, 256), dtype=np.uint64)
+    shifts = np.arange(3, 64)
+    for i in range(nu):
+        pos = rng.choice(256, size=3, replace=False)
+        for k, p in enumerate(pos):
+            s = int(shifts[(3 * i + k) % len(shifts)])
+            blocks[i, p] = np.uint64((1 << s) | int(rng.integers(0, 1 << min(s, 62))))
+    exp_packed, exp_off = oracle_lib.enc256v64_batch(blocks)
+    packed, offs = tpf.enc_batch("256v64", to_dev(blocks.ravel(), True), nu, 256)
+    np.testing.assert_array_equal(offs.cpu().numpy().astype(np.uint64), exp_off)
+    np.testing.assert_array_equal(packed.cpu().numpy(), exp_packed)
+    heads = exp_packed[exp_off[:-1].astype(np.int64)]
+    assert int(((heads & 0xC0) == 0x40).sum()) > nu // 2, "vbyte mode not chosen"
+    out = tpf.dec_batch("256v64", packed, offs, nu, 256)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint64).reshape(-1, 256), blocks)
+    # the same exceptions through D1 (gaps = the blocks' values)
+    vals = np.cumsum(blocks.ravel() + np.uint64(1), dtype=np.uint64).reshape(nu, 256) - np.uint64(1)
+    starts = np.zeros(nu, dtype=np.uint64)
+    starts[1:] = vals[:-1, -1]
+    exp_packed, exp_off = oracle_lib.enc256v64_batch(vals, starts=starts)
+    packed, offs = tpf.enc_batch("256v64", to_dev(vals.ravel(), True), nu, 256, d1=True, start0=0)
+    np.testing.assert_array_equal(packed.cpu().numpy(), exp_packed)
+    out = tpf.dec_batch("256v64", packed, offs, nu, 256, starts=to_dev(starts, True))
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint64).reshape(-1, 256), vals)
