@@ -74,6 +74,11 @@ int tpf_perblock_mode(int mode);
  * host-memory mailboxes of mode 2. */
 void tpf_perblock_quiesce(void);
 
+/* Diagnostics: launches of the block server since the process started (every
+ * device).  A launch serves until it has been idle for 10 ms, or for 5 ms of
+ * service at most; calls/launch shows whether it leaves early. */
+uint64_t tpf_perblock_launches(void);
+
 /* ---- stream framing (host, no decoding) -------------------
  * Encoded length of the block at `in` (fmt = TPF_FMT_*, n = values per call),
  * reading at most `avail` bytes; 0 if malformed/truncated.  values_written
@@ -99,9 +104,12 @@ int64_t tpf_check_offsets(const uint64_t *off, uint64_t nblocks, uint64_t in_byt
  * host copies -- the library never page-locks caller memory.  Staging buffers and
  * streams are pooled per device across calls; tpf_host_release() frees them.
  * h_off may be NULL for decode (offsets are scanned with tpf_scan_offsets);
- * given offsets must not decrease and must end at or below in_bytes
- * (TPF_EINVAL otherwise), and a block whose parsed length disagrees with its
- * offsets fails the call with TPF_ECORRUPT (tpf_last_error names the block).
+ * given offsets have nblocks + 1 readable entries (the length cannot be
+ * checked: a shorter array is an out-of-bounds host read), must not decrease
+ * and must end at or below in_bytes (TPF_EINVAL otherwise, checked on the host
+ * before any device is touched), and a block whose parsed length disagrees
+ * with its offsets fails the call with TPF_ECORRUPT (tpf_last_error names the
+ * block).  Encode writes nblocks + 1 entries to h_off.
  * Encode fails with TPF_EINVAL when the blocks do not fit in out_cap.
  * Value arrays use the unit strides documented in turbopfor_gpu.h. */
 int tpf_host_dec(int fmt, const uint8_t *h_in, uint64_t in_bytes, const uint64_t *h_off, uint64_t nblocks, unsigned n,

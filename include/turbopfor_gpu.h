@@ -10,8 +10,16 @@
  *     pointer (README.md:108-123);
  *   - d_off[0..nblocks] are byte offsets of each block (d_off[nblocks] = end);
  *     the reference has no offsets (block sizes are implicit), so the batch
- *     encoders produce them and tpf_scan_blocks* recovers them from a legacy
+ *     encoders produce them and tpf_scan_offsets recovers them from a legacy
  *     stream;
+ *   - OFFSETS CONTRACT (every entry below that takes d_off / h_off): the
+ *     array has nblocks + 1 readable entries.  The kernels read d_off[i] and
+ *     d_off[i+1] of every block they decode; the array's length is not passed
+ *     and cannot be checked on the device, so a shorter array is an
+ *     out-of-bounds device read (round 5 saw one fault from a test that broke
+ *     this).  The VALUES are checked: an offset outside [0, in_bytes] or a
+ *     block whose parse disagrees with its offsets is reported through d_err,
+ *     never followed;
  *   - decoded values are nblocks * 256 contiguous integers.
  * No device-side slack is required: all device reads are bounds-checked
  * against in_bytes.

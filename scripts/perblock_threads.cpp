@@ -20,6 +20,10 @@
 #include "turbopfor.h"
 #include "turbopfor_capi.h"
 
+// weak: the tool also runs against older library builds without the counter
+#pragma weak tpf_perblock_launches
+static uint64_t launches_now() { return tpf_perblock_launches ? tpf_perblock_launches() : 0; }
+
 static void fill_block(uint32_t * v, uint32_t seed)
 {
     // bw 8 base with 10% exceptions in [2^8, 2^32): the ab_test-style mix (ab_test.cpp:1611-1626)
@@ -59,6 +63,7 @@ int main(int argc, char ** argv)
         const int T = std::atoi(argv[a]);
         std::atomic<int> bad{0};
         double dec_s = 0, enc_s = 0;
+        uint64_t launches[2] = {0, 0}; // block-server launches during each timed phase
         for (int phase = 0; phase < 2; ++phase) // 0 = encode, 1 = decode
         {
             std::atomic<int> ready{0};
@@ -96,19 +101,21 @@ int main(int argc, char ** argv)
                 });
             while (ready.load() + bad.load() < T)
                 std::this_thread::yield();
+            const uint64_t l0 = launches_now();
             const auto t0 = std::chrono::steady_clock::now();
             go = true;
             for (auto & t : th)
                 t.join();
             const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            launches[phase] = launches_now() - l0;
             (phase == 0 ? enc_s : dec_s) = wall;
         }
         const double calls = static_cast<double>(T) * K;
         std::printf("{\"mode\": %d, \"n\": %u, \"threads\": %d, \"calls_per_thread\": %d, \"dec_calls_per_s\": %.0f, \"dec_G_int32_per_s\": %.4f, "
                     "\"dec_us_per_call\": %.2f, \"enc_calls_per_s\": %.0f, \"enc_G_int32_per_s\": %.4f, \"enc_us_per_call\": %.2f, "
-                    "\"bad\": %d}\n",
+                    "\"enc_launches\": %llu, \"dec_launches\": %llu, \"bad\": %d}\n",
                     mode, nv, T, K, calls / dec_s, calls * (nv >= 256u ? 256u : nv) / dec_s / 1e9, dec_s * T / calls * 1e6, calls / enc_s, calls * (nv >= 256u ? 256u : nv) / enc_s / 1e9,
-                    enc_s * T / calls * 1e6, bad.load());
+                    enc_s * T / calls * 1e6, static_cast<unsigned long long>(launches[0]), static_cast<unsigned long long>(launches[1]), bad.load());
         std::fflush(stdout);
         if (bad.load())
             return 1;

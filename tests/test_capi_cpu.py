@@ -122,3 +122,33 @@ def test_nested_perblock_pauses(lib, tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "pause nesting ok" in r.stdout
+
+
+def test_host_entries_check_offsets_before_the_device(lib):
+    """h_off has nblocks + 1 entries (turbopfor_capi.h).  The
+    host entries cannot see the array's length, but they reject what a short
+    or foreign array yields -- offsets that decrease or run past in_bytes --
+    and a bad (fmt, n) with TPF_EINVAL, on the host, before any device is
+    touched: the same answer with or without a GPU."""
+    lib.tpf_last_error.restype = ctypes.c_char_p
+    lib.tpf_host_dec.restype = ctypes.c_int
+    lib.tpf_host_dec_multi.restype = ctypes.c_int
+    data = (ctypes.c_uint8 * 4096)()
+    vals = (ctypes.c_uint32 * (256 * 4))()
+    devs = (ctypes.c_int * 2)(0, 0)
+    u64 = ctypes.c_uint64
+    cases = [
+        ((ctypes.c_uint64 * 5)(0, 10, 20, 30, 5000), b"past in_bytes"),   # ends past the 4096-byte stream
+        ((ctypes.c_uint64 * 5)(0, 10, 5, 30, 40), b"decreases at block 1"),
+        ((ctypes.c_uint64 * 5)(0, 10, 20, 30, 2 ** 63), b"past in_bytes"),  # garbage read past a short array
+    ]
+    for off, msg in cases:
+        assert lib.tpf_host_dec(2, data, u64(4096), off, u64(4), 256, vals, None) == -1
+        assert msg in lib.tpf_last_error(), lib.tpf_last_error()
+        assert lib.tpf_host_dec_multi(devs, 2, 2, data, u64(4096), off, u64(4), 256, vals, None) == -1
+        assert msg in lib.tpf_last_error(), lib.tpf_last_error()
+    good = (ctypes.c_uint64 * 5)(0, 10, 20, 30, 40)
+    assert lib.tpf_host_dec(2, data, u64(4096), good, u64(4), 300, vals, None) == -1  # n past the 256v32 unit
+    assert b"unsupported" in lib.tpf_last_error()
+    assert lib.tpf_host_dec(2, None, u64(4096), good, u64(4), 256, vals, None) == -1
+    assert lib.tpf_host_dec_multi(None, 0, 2, data, u64(4096), good, u64(4), 256, vals, None) == -1

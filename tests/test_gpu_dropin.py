@@ -288,10 +288,11 @@ def test_host_streams_of_two_threads_overlap():
     assert max(a0, b0) < min(a1, b1), f"calls ran one after the other: {spans}"
 
 
-@pytest.mark.parametrize("nthreads", [16, 80])
+@pytest.mark.parametrize("nthreads", [16, 80, 128])
 def test_per_block_server_concurrent_threads(nthreads):
-    """16 threads (each its own mailbox) and 80 (more than the server's 64
-    mailboxes: callers wait for a free one) call at once: every thread's
+    """16 threads (each its own mailbox), 80 and 128 (more than the server's
+    64 mailboxes: callers are admitted through the mailbox semaphore and, with
+    more threads than CPUs, sleep while they wait) call at once: every thread's
     encode -> decode round trip of its own blocks is byte-exact (oracle),
     bit-exact, and every returned end pointer is right."""
     import threading
@@ -644,3 +645,47 @@ def test_device_synchronize_beside_busy_per_block_caller():
     assert calls[0] > 0
     assert dt < 10.0, f"20 device-wide synchronizes took {dt:.1f} s beside a busy per-block caller"
     assert int(x[0].item()) == 20
+
+
+def test_block_server_launches_track_its_lifetime():
+    """the idle-exit test could wrap (the clock read before another
+    workgroup published a later activity time) and end the whole server early.
+    A launch now leaves only after 10 ms idle, after its 5 ms lifetime, or
+    when stopped: under continuous calls from 8 threads for ~0.3 s the
+    launches stay within the lifetime's count (plus slack for the first
+    launch and the relaunch gaps)."""
+    import threading
+    import time
+
+    L = capi()
+    L.tpf_p4Enc256v32.restype = ctypes.c_void_p
+    L.tpf_p4Enc256v32.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]
+    L.tpf_perblock_launches.restype = ctypes.c_uint64
+    v = np.ascontiguousarray(datagen.c2_blocks(1, 9, 10, seed=3)[0])
+    buf0 = np.zeros(4096, np.uint8)
+    assert L.tpf_p4Enc256v32(v.ctypes.data, 256, buf0.ctypes.data) is not None  # server up
+    stop = time.monotonic() + 0.3
+    calls = [0] * 8
+    errors = []
+
+    def worker(k):
+        buf = np.zeros(4096, np.uint8)
+        try:
+            while time.monotonic() < stop:
+                assert L.tpf_p4Enc256v32(v.ctypes.data, 256, buf.ctypes.data) is not None
+                calls[k] += 1
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    l0 = L.tpf_perblock_launches()
+    t0 = time.monotonic()
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=60)
+    dt = time.monotonic() - t0
+    launches = L.tpf_perblock_launches() - l0
+    assert not errors, errors
+    assert sum(calls) > 100
+    assert launches <= dt / 0.005 * 1.25 + 4, (launches, dt, sum(calls))

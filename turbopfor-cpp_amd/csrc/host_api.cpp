@@ -19,6 +19,9 @@
 // (device-resident batches).
 #include <hip/hip_runtime.h>
 #include <immintrin.h>
+#include <sched.h>
+#include <sys/prctl.h>
+#include <time.h>
 
 #include <algorithm>
 #include <atomic>
@@ -26,7 +29,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <mutex>
+#include <semaphore>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -165,10 +170,112 @@ struct Ctx
     ~Ctx() { reset(); }
 };
 
+// ---- waiting for an answer: spin, or sleep when callers outnumber CPUs ------
+// Round 6.  A waiting caller spun on its answer word.  With
+// more calling threads than CPUs the spinners took the CPUs from the threads
+// that would post requests and read answers; on a machine whose CPU time is
+// capped by a cgroup quota (the GPU boxes: 256 visible CPUs, 16 CPUs of
+// quota) every spinner sits on a CPU of its own and burns quota, the cgroup is
+// throttled for the rest of each period, and the aggregate collapsed (64
+// callers: 1.17M calls/s at 55 us per call, against 3.8M at 24).  Yielding
+// does not help there (a thread alone on its CPU gets it straight back).  So
+// when the threads that call the library outnumber the CPUs the process may
+// use, a waiter sleeps between polls instead (1 us of timer slack on the
+// calling thread, set once); otherwise it spins as before.
+
+// CPUs this process may use: its affinity mask, capped by a cgroup CPU quota
+// (v2 cpu.max, v1 cfs_quota_us / cfs_period_us).
+unsigned effective_cpus()
+{
+    cpu_set_t set;
+    unsigned n = 0;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0)
+        n = static_cast<unsigned>(CPU_COUNT(&set));
+    if (n == 0)
+        n = std::max(1u, std::thread::hardware_concurrency());
+    double quota = -1, period = -1;
+    {
+        std::ifstream f("/sys/fs/cgroup/cpu.max");
+        std::string q;
+        if (f >> q >> period && q != "max")
+            quota = std::atof(q.c_str());
+    }
+    if (quota <= 0)
+    {
+        std::ifstream fq("/sys/fs/cgroup/cpu/cpu.cfs_quota_us"), fp("/sys/fs/cgroup/cpu/cpu.cfs_period_us");
+        if (!(fq >> quota && fp >> period))
+            quota = -1;
+    }
+    if (quota > 0 && period > 0)
+        n = std::min(n, std::max(1u, static_cast<unsigned>(quota / period + 0.999)));
+    return n;
+}
+
+// Threads that have made a per-block call and still exist (each registers on
+// its first call, deregisters at exit): the one word a call reads for the
+// policy is written only when threads come and go.
+std::atomic<unsigned> g_callers{0};
+struct CallerReg
+{
+    bool on = false;
+    void enter()
+    {
+        if (!on)
+        {
+            on = true;
+            g_callers.fetch_add(1u, std::memory_order_relaxed);
+        }
+    }
+    ~CallerReg()
+    {
+        if (on)
+            g_callers.fetch_sub(1u, std::memory_order_relaxed);
+    }
+};
+
+// TPF_PERBLOCK_WAIT=spin / sleep forces one policy (A/B runs); default: auto.
+int wait_policy()
+{
+    const char * e = std::getenv("TPF_PERBLOCK_WAIT");
+    if (e && std::strcmp(e, "spin") == 0)
+        return 1;
+    if (e && std::strcmp(e, "sleep") == 0)
+        return 2;
+    return 0;
+}
+
+// calling threads (registers the calling thread)
+unsigned callers()
+{
+    thread_local CallerReg reg;
+    reg.enter();
+    return g_callers.load(std::memory_order_relaxed);
+}
+
+bool crowded()
+{
+    static const unsigned cpus = effective_cpus();
+    static const int policy = wait_policy();
+    return policy == 2 || (policy == 0 && callers() > cpus);
+}
+
+void nap_ns(long ns)
+{
+    thread_local bool slack = [] {
+        (void)prctl(PR_SET_TIMERSLACK, 1000ul, 0ul, 0ul, 0ul); // 1 us (the default 50 us would set every nap's length)
+        return true;
+    }();
+    (void)slack;
+    timespec ts{0, ns};
+    (void)nanosleep(&ts, nullptr);
+}
+
 // ---- resident block server (per device) ------------------------------------
 // 0 = block server with request mailboxes in device memory, 1 = launch +
 // synchronise per call, 2 = block server with request mailboxes in host memory
 std::atomic<int> g_mode{0};
+// launches of the block server on every device (tpf_perblock_launches)
+std::atomic<uint64_t> g_launches{0};
 
 struct Server
 {
@@ -201,6 +308,11 @@ struct Server
     };
     Box box[tpf::kServerBoxes];
     bool held = false; // every mailbox taken by the pause (pause thread only)
+    // With more calling threads than mailboxes, callers are admitted through
+    // this semaphore first (a futex wait, no CPU), so that at most one caller
+    // per mailbox searches the lock words: 128 threads scanning 64 lines
+    // between naps served 0.9M calls/s (r6b).
+    std::counting_semaphore<tpf::kServerBoxes> gate{tpf::kServerBoxes};
 
     static void * pinned(size_t bytes, void ** dev_view)
     {
@@ -255,6 +367,7 @@ struct Server
         hip_check(tpf::launch_block_server(rq == rq_host ? rq_host_d : rq, an_d, ctl, stream), "block server launch");
         hip_check(hipEventRecord(done, stream), "block server event");
         launched = true;
+        g_launches.fetch_add(1u, std::memory_order_relaxed);
         launched_rq.store(rq, std::memory_order_release);
     }
     // caller holds mu: has the current launch ended (idle exit or stop)?
@@ -320,7 +433,11 @@ struct Server
                 if (try_lease(i))
                     return static_cast<int>(i);
             }
-            std::this_thread::yield();
+            // more callers than mailboxes: wait without burning CPU when crowded
+            if (crowded())
+                nap_ns(2000);
+            else
+                std::this_thread::yield();
         }
     }
     void release(int i) { box[i].busy.store(0u, std::memory_order_release); }
@@ -363,13 +480,30 @@ struct Server
         std::atomic_thread_fence(std::memory_order_release);
         __atomic_store_n(&b->req, r, __ATOMIC_RELEASE);
         _mm_sfence();
+        // Spin (a call takes ~5 us), or with more calling threads than CPUs
+        // sleep between polls (see crowded()); a spinner that has waited
+        // kSpinNs -- over twice a call's latency -- yields between polls.
+        constexpr auto kSpinNs = std::chrono::nanoseconds(12000);
+        const bool crowd = crowded();
         const auto t0 = std::chrono::steady_clock::now();
+        bool patient = false;
+        if (crowd)
+            nap_ns(3000);
         for (uint64_t spin = 1;; ++spin)
         {
             if (__atomic_load_n(&a->ack, __ATOMIC_ACQUIRE) == r)
                 break;
-            _mm_pause();
-            if ((spin & 1023u) == 0u)
+            if (crowd)
+                nap_ns(1000);
+            else if (patient)
+                std::this_thread::yield();
+            else
+            {
+                _mm_pause();
+                if ((spin & 31u) == 0u && std::chrono::steady_clock::now() - t0 > kSpinNs)
+                    patient = true;
+            }
+            if ((spin & (crowd || patient ? 15u : 1023u)) == 0u)
             {
                 // the launch may have idled out just before this request:
                 // relaunch.  Only when it shows signs of having ended (alive
@@ -485,8 +619,14 @@ struct BoxLease
     tpf::ServerReq * rq;
     int i = 0;
     bool own = false;
+    bool gated = false;
     explicit BoxLease(Server & srv) : s(srv), rq(nullptr)
     {
+        if (t_pause_depth == 0 && callers() > tpf::kServerBoxes)
+        {
+            s.gate.acquire();
+            gated = true;
+        }
         if (t_pause_depth == 0)
             for (;;)
             {
@@ -504,6 +644,8 @@ struct BoxLease
     {
         if (own)
             s.release(i);
+        if (gated)
+            s.gate.release();
     }
     tpf::ServerReqBox * req() const { return &rq->box[i]; }
     tpf::ServerAnsBox * ans() const { return &s.an->box[i]; }
@@ -779,6 +921,8 @@ void tpf_perblock_quiesce(void)
 {
     const tpf::PerblockPause p; // nests inside a pause this thread already holds
 }
+
+uint64_t tpf_perblock_launches(void) { return g_launches.load(std::memory_order_relaxed); }
 
 int tpf_perblock_mode(int mode)
 {

@@ -31,6 +31,7 @@
 
 #include "../../include/turbopfor_capi.h"
 #include "../../include/turbopfor_gpu.h"
+#include "shard_exec.h"
 #include "tpf_kernels.h"
 
 namespace tpf
@@ -296,32 +297,35 @@ struct Pipeline
     }
 };
 
-std::mutex g_pool_mu;
-std::vector<Pipeline *> g_pool; // idle pipelines (any device)
+// The device discipline of the pool and of the shard threads lives in
+// shard_exec.h (HIP-free, driven by a mock device map in
+// tests/cpp/shard_exec_mock.cpp); these are its HIP operations.
+struct HipOps
+{
+    int get_dev()
+    {
+        int d = 0;
+        hc(hipGetDevice(&d), "hipGetDevice");
+        return d;
+    }
+    bool set_dev(int d) { return hipSetDevice(d) == hipSuccess; }
+    Pipeline * make(int d) { return new Pipeline(d); } // streams, events and buffers of the current device d
+};
 
-// Exclusive use of a pooled pipeline for one call; on return the streams are
-// drained and the pipeline goes back to the pool (or is dropped after an
-// error, when its state is unknown).
+tpf::DevicePool<Pipeline> g_pool; // idle pipelines, keyed by device
+
+// Exclusive use of a pooled pipeline of the calling thread's device for one
+// call; on return the streams are drained and the pipeline goes back to the
+// pool (or is destroyed -- with its own device selected -- after an error,
+// when its state is unknown).
 struct Lease
 {
     Pipeline * p = nullptr;
     bool ok = false;
     Lease()
     {
-        int dev = 0;
-        hc(hipGetDevice(&dev), "hipGetDevice");
-        {
-            std::lock_guard<std::mutex> g(g_pool_mu);
-            for (size_t i = 0; i < g_pool.size(); ++i)
-                if (g_pool[i]->dev == dev)
-                {
-                    p = g_pool[i];
-                    g_pool.erase(g_pool.begin() + static_cast<std::ptrdiff_t>(i));
-                    break;
-                }
-        }
-        if (!p)
-            p = new Pipeline(dev);
+        HipOps ops;
+        p = g_pool.acquire(ops);
         for (Slot & s : p->slots)
             s.pend = Slot::Pending{};
     }
@@ -329,14 +333,18 @@ struct Lease
     {
         const bool drained = hipStreamSynchronize(p->ks) == hipSuccess && hipStreamSynchronize(p->cs) == hipSuccess;
         if (ok && drained)
-        {
-            std::lock_guard<std::mutex> g(g_pool_mu);
-            g_pool.push_back(p);
-        }
+            g_pool.give_back(p);
         else
         {
             const FreePause fp;
-            delete p;
+            HipOps ops;
+            try
+            {
+                tpf::DevicePool<Pipeline>::destroy(ops, p);
+            }
+            catch (...)
+            {
+            }
         }
     }
 };
@@ -382,7 +390,15 @@ int host_dec_impl(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64
     {
         if (nblocks == 0)
             return TPF_OK;
-        need_device();
+        // The arguments are checked on the host before anything touches a
+        // device (round 6: the same answer with or without a GPU).
+        // h_off has nblocks + 1 entries (turbopfor_capi.h): a shorter array
+        // cannot be detected, but what it usually yields -- offsets that
+        // decrease or run past in_bytes -- is rejected here, before any copy.
+        if (!h_in || !h_vals)
+            throw Err(TPF_EINVAL, "tpf_host_dec: null pointer");
+        if (!tpf::fmt_ok(fmt, n))
+            throw Err(TPF_EINVAL, "tpf_host_dec: unsupported (fmt, n)");
         std::vector<uint64_t> scanned;
         if (!h_off)
         {
@@ -400,6 +416,7 @@ int host_dec_impl(int fmt, const uint8_t * h_in, uint64_t in_bytes, const uint64
             if (bad < 0)
                 throw Err(TPF_EINVAL, "tpf_host_dec: h_off decreases at block " + std::to_string(-bad - 1));
         }
+        need_device();
         const size_t es = wide_fmt(fmt) ? 8 : 4;
         const size_t uv = unit_values(fmt, n);
         const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(nblocks, chunk_value_bytes() / (es * uv)));
@@ -517,14 +534,12 @@ int tpf_host_dec_multi(const int * devs, int ndev, int fmt, const uint8_t * h_in
     {
         if (nblocks == 0)
             return TPF_OK;
-        need_device();
-        int cnt = 0;
-        hc(hipGetDeviceCount(&cnt), "hipGetDeviceCount");
         if (!devs || ndev < 1 || ndev > 64)
             throw Err(TPF_EINVAL, "tpf_host_dec_multi: need 1..64 devices");
-        for (int d = 0; d < ndev; ++d)
-            if (devs[d] < 0 || devs[d] >= cnt)
-                throw Err(TPF_EINVAL, "tpf_host_dec_multi: device " + std::to_string(devs[d]) + " is not visible");
+        if (!h_in || !h_vals)
+            throw Err(TPF_EINVAL, "tpf_host_dec_multi: null pointer");
+        if (!tpf::fmt_ok(fmt, n))
+            throw Err(TPF_EINVAL, "tpf_host_dec_multi: unsupported (fmt, n)");
         std::vector<uint64_t> scanned;
         if (!h_off)
         {
@@ -541,6 +556,12 @@ int tpf_host_dec_multi(const int * devs, int ndev, int fmt, const uint8_t * h_in
             if (bad < 0)
                 throw Err(TPF_EINVAL, "tpf_host_dec_multi: h_off decreases at block " + std::to_string(-bad - 1));
         }
+        need_device();
+        int cnt = 0;
+        hc(hipGetDeviceCount(&cnt), "hipGetDeviceCount");
+        for (int d = 0; d < ndev; ++d)
+            if (devs[d] < 0 || devs[d] >= cnt)
+                throw Err(TPF_EINVAL, "tpf_host_dec_multi: device " + std::to_string(devs[d]) + " is not visible");
         const size_t es = wide_fmt(fmt) ? 8 : 4;
         const size_t uv = unit_values(fmt, n);
         // shard cuts: equal shares of the stream's bytes (block granularity)
@@ -552,32 +573,25 @@ int tpf_host_dec_multi(const int * devs, int ndev, int fmt, const uint8_t * h_in
             const uint64_t target = h_off[0] + total / static_cast<uint64_t>(ndev) * static_cast<uint64_t>(d);
             cut[d] = std::max<uint64_t>(cut[d - 1], static_cast<uint64_t>(std::lower_bound(h_off, h_off + nblocks, target) - h_off));
         }
-        std::vector<int> rc(static_cast<size_t>(ndev), TPF_OK);
-        std::vector<std::string> msg(static_cast<size_t>(ndev));
-        std::vector<std::thread> th;
-        for (int d = 0; d < ndev; ++d)
-            th.emplace_back([&, d] {
+        // one thread per shard, bound to its device first (shard_exec.h)
+        const std::vector<tpf::ShardResult> res = tpf::run_shards(
+            devs, ndev, [](int dev) { return hipSetDevice(dev) == hipSuccess; },
+            [&](int d, std::string & msg) {
                 const uint64_t b0 = cut[d], nb = cut[d + 1] - cut[d];
                 if (nb == 0)
-                    return;
-                if (hipSetDevice(devs[d]) != hipSuccess)
-                {
-                    rc[d] = TPF_EHIP;
-                    msg[d] = "hipSetDevice failed";
-                    return;
-                }
-                rc[d] = host_dec_impl(fmt, h_in, in_bytes, h_off + b0, nb, n, static_cast<uint8_t *>(h_vals) + b0 * uv * es,
-                                      h_starts ? static_cast<const uint8_t *>(h_starts) + b0 * es : nullptr);
-                if (rc[d] != TPF_OK)
-                    msg[d] = tpf_last_error(); // thread-local: carried to the caller's thread below
-            });
-        for (std::thread & t : th)
-            t.join();
+                    return TPF_OK;
+                const int rc = host_dec_impl(fmt, h_in, in_bytes, h_off + b0, nb, n, static_cast<uint8_t *>(h_vals) + b0 * uv * es,
+                                             h_starts ? static_cast<const uint8_t *>(h_starts) + b0 * es : nullptr);
+                if (rc != TPF_OK)
+                    msg = tpf_last_error(); // thread-local: carried to the caller's thread below
+                return rc;
+            },
+            TPF_EHIP, TPF_EHIP);
         for (int d = 0; d < ndev; ++d)
-            if (rc[d] != TPF_OK)
-                throw Err(rc[d], "tpf_host_dec_multi: shard " + std::to_string(d) + " (device " + std::to_string(devs[d]) + ", blocks " +
-                                     std::to_string(cut[d]) + ".." + std::to_string(cut[d + 1]) + ", block numbers below are shard-relative): " +
-                                     msg[d]);
+            if (res[d].rc != TPF_OK)
+                throw Err(res[d].rc, "tpf_host_dec_multi: shard " + std::to_string(d) + " (device " + std::to_string(devs[d]) + ", blocks " +
+                                         std::to_string(cut[d]) + ".." + std::to_string(cut[d + 1]) +
+                                         ", block numbers below are shard-relative): " + res[d].msg);
         return TPF_OK;
     }
     catch (const Err & e)
@@ -752,20 +766,12 @@ int tpf_host_enc_multi(const int * devs, int ndev, int fmt, const void * h_vals,
         const bool in_place = prov[ndev] <= out_cap;
         std::vector<std::unique_ptr<uint8_t[]>> tmp(static_cast<size_t>(ndev));
         std::vector<std::vector<uint64_t>> toff(static_cast<size_t>(ndev));
-        std::vector<int> rc(static_cast<size_t>(ndev), TPF_OK);
-        std::vector<std::string> msg(static_cast<size_t>(ndev));
-        std::vector<std::thread> th;
-        for (int d = 0; d < ndev; ++d)
-            th.emplace_back([&, d] {
+        const std::vector<tpf::ShardResult> res = tpf::run_shards(
+            devs, ndev, [](int dev) { return hipSetDevice(dev) == hipSuccess; },
+            [&](int d, std::string & msg) {
                 const uint64_t b0 = cut[d], nb = cut[d + 1] - cut[d];
                 if (nb == 0)
-                    return;
-                if (hipSetDevice(devs[d]) != hipSuccess)
-                {
-                    rc[d] = TPF_EHIP;
-                    msg[d] = "hipSetDevice failed";
-                    return;
-                }
+                    return TPF_OK;
                 // a chained D1 list (no per-unit starts): shard d starts after the
                 // previous unit's value n-1 (slots past n are padding)
                 uint64_t s0 = start0;
@@ -775,38 +781,30 @@ int tpf_host_enc_multi(const int * devs, int ndev, int fmt, const void * h_vals,
                     std::memcpy(&s0, vals + ((b0 - 1) * uv + n - 1) * es, es);
                 }
                 const void * st = (d1 && h_starts) ? static_cast<const uint8_t *>(h_starts) + b0 * es : nullptr;
+                int rc;
                 if (d == 0)
-                    rc[d] = tpf_host_enc(fmt, vals, nb, n, d1, st, s0, h_out, out_cap, h_off);
+                    rc = tpf_host_enc(fmt, vals, nb, n, d1, st, s0, h_out, out_cap, h_off);
                 else
                 {
                     const uint64_t cap = prov[d + 1] - prov[d];
                     uint8_t * dst = h_out + prov[d];
-                    try
+                    if (!in_place)
                     {
-                        if (!in_place)
-                        {
-                            tmp[d].reset(new uint8_t[cap]);
-                            dst = tmp[d].get();
-                        }
-                        toff[d].resize(nb + 1);
+                        tmp[d].reset(new uint8_t[cap]); // (a bad_alloc is recorded for this shard by run_shards)
+                        dst = tmp[d].get();
                     }
-                    catch (const std::exception & e)
-                    {
-                        rc[d] = TPF_EHIP;
-                        msg[d] = e.what();
-                        return;
-                    }
-                    rc[d] = tpf_host_enc(fmt, vals + b0 * uv * es, nb, n, d1, st, s0, dst, cap, toff[d].data());
+                    toff[d].resize(nb + 1);
+                    rc = tpf_host_enc(fmt, vals + b0 * uv * es, nb, n, d1, st, s0, dst, cap, toff[d].data());
                 }
-                if (rc[d] != TPF_OK)
-                    msg[d] = tpf_last_error(); // thread-local: carried to the caller's thread below
-            });
-        for (std::thread & t : th)
-            t.join();
+                if (rc != TPF_OK)
+                    msg = tpf_last_error(); // thread-local: carried to the caller's thread below
+                return rc;
+            },
+            TPF_EHIP, TPF_EHIP);
         for (int d = 0; d < ndev; ++d)
-            if (rc[d] != TPF_OK)
-                throw Err(rc[d], "tpf_host_enc_multi: shard " + std::to_string(d) + " (device " + std::to_string(devs[d]) + ", blocks " +
-                                     std::to_string(cut[d]) + ".." + std::to_string(cut[d + 1]) + "): " + msg[d]);
+            if (res[d].rc != TPF_OK)
+                throw Err(res[d].rc, "tpf_host_enc_multi: shard " + std::to_string(d) + " (device " + std::to_string(devs[d]) + ", blocks " +
+                                         std::to_string(cut[d]) + ".." + std::to_string(cut[d + 1]) + "): " + res[d].msg);
         // move the later shards into place behind the earlier ones, in order
         // (each destination ends at or before its provisional source)
         for (int d = 1; d < ndev; ++d)
@@ -841,13 +839,15 @@ int tpf_host_enc_multi(const int * devs, int ndev, int fmt, const void * h_vals,
 void tpf_host_release(void)
 {
     const FreePause fp; // the frees below wait on every stream of the device
-    std::vector<Pipeline *> idle;
+    HipOps ops;
+    try
     {
-        std::lock_guard<std::mutex> g(g_pool_mu);
-        idle.swap(g_pool);
+        g_pool.drain(ops); // each pipeline destroyed with its own device selected
     }
-    for (Pipeline * p : idle)
-        delete p;
+    catch (const std::exception & e)
+    {
+        tpf::set_last_error(e.what());
+    }
 }
 
 } // extern "C"

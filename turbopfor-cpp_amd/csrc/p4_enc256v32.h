@@ -36,7 +36,7 @@
 namespace tpf::dev
 {
 
-constexpr uint32_t kImgU32 = 592; // bytes per wave image: 4..7 lead + block (<= 2276 B) + slack, 16-B multiple
+constexpr uint32_t kImgU32 = kImgU32Max; // dwords per wave image: 4..7 lead + block (<= 2276 B) + slack, 16-B multiple
 constexpr uint32_t kEncRun = 16;  // blocks per wave run (the workspace is sized for it)
 // D1 encodes (posting lists: small blocks) run 32 blocks per wave: C3 D1
 // encode +2%, while the plain C4 mix loses 0.8% with 32 (r5ab)
@@ -181,42 +181,61 @@ __device__ __forceinline__ void plan_run(const Run & R, const uint32_t * in, con
     });
 }
 
-// Write a run: lane j of (szv, pwv, olo/ohi) = size, plan word and byte
-// offset of block R.first+j.  img: the wave's zeroed LDS image (left zeroed).
+// Write a run: lane j of (szv, pwv, ov) = size, plan word and byte offset of
+// block R.first+j.  img: the wave's zeroed LDS image (left zeroed).  Round 6:
+// the blocks' layouts come from a run plane (enc_geo, one vector pass per
+// run) and the copy-out goes through one buffer descriptor per run
+// (RunCopyB): the per-block scalar work of round 5's form -- 136 SALU and 29
+// branches per C3 block against 141 VALU, on the CU's one scalar unit -- is
+// gone.
 template <bool D1, int PROBE = 0, class Run>
 __device__ __forceinline__ void write_run(const Run & R, const uint32_t * in, const uint32_t * starts, uint32_t start0,
-                                          uint32_t szv, uint32_t pwv, uint32_t olo, uint32_t ohi, uint32_t * img,
-                                          uint32_t * val, uint64_t out_base, uint64_t cap_end, uint32_t t)
+                                          uint32_t szv, uint32_t pwv, uint64_t ov, uint32_t * img, uint32_t * val,
+                                          uint64_t out_base, uint64_t cap_end, uint32_t t)
 {
     const uint32_t stv = D1 ? R.start_lane(in, starts, start0, t) : 0u;
-    RunCopy rc;
-    R.template walk<kEncNCWrite>(t, [&](u32x4 v, uint32_t jj) {
-        if constexpr (D1)
-            v = delta_encode(v, rl32(stv, jj), t);
-        const uint32_t size = rl32(szv, jj);
-        const Plan32 P = unplan(rl32(pwv, jj), size);
-        const uint64_t dst = out_base + ((static_cast<uint64_t>(rl32(ohi, jj)) << 32) | rl32(olo, jj));
-        if constexpr (PROBE == 2)
-        {
+    if constexpr (PROBE == 2)
+    {
+        R.template walk<kEncNCWrite>(t, [&](u32x4 v, uint32_t jj) {
+            const uint32_t size = rl32(szv, jj);
+            const uint64_t dst = out_base + readlane_u64(ov, jj);
             reinterpret_cast<u32x4 *>(img)[4 + t] = v;
             wave_lds_sync();
             copy_out_image16(img, kImgLead, dst, size, cap_end, t);
             wave_lds_sync();
             zero_image(img, kImgU32 / 4u, t);
             wave_lds_sync();
-            return;
-        }
-        const uint32_t sb = emit_block256<true>(img, val, P, v, t);
+        });
+        return;
+    }
+    (void)cap_end; // the batch entry points require out_cap >= the bound: no chunk passes the stream's end
+    // the run's output through one descriptor based at its first byte rounded down to 16
+    const uint64_t ab = out_base + ov;
+    const uint64_t A = readlane_u64(ab, 0) & ~15ull;
+    const uint32_t rel = static_cast<uint32_t>(ab - A);
+    const uint32_t lead = rl32(rel, 0); // < 16
+    const uint32_t rel_end = rl32(rel + szv, R.n - 1u);
+    RunCopyB rc;
+    rc.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(A), static_cast<short>(0), static_cast<int>(rel_end), 0x00020000);
+    // the block that completes the run's partial first chunk stores its bytes [lead, 16)
+    const uint64_t flush = __builtin_amdgcn_ballot_w64(t < R.n && lead != 0u && rel < 16u && rel + szv >= 16u);
+    const uint32_t trash_at = static_cast<uint32_t>(reinterpret_cast<uint8_t *>(val + kEncTrash + t) - reinterpret_cast<uint8_t *>(img));
+    R.template walk<kEncNCWrite>(t, [&](u32x4 v, uint32_t jj) {
+        if constexpr (D1)
+            v = delta_encode(v, rl32(stv, jj), t);
+        // the layout from three values read per block (the plan word, size and
+        // output byte), derived on the scalar unit: eighteen v_readlane of a
+        // full run plane cost more VALU cycles and 19 VGPRs (6 waves per SIMD
+        // instead of 8) than the scalar derivation (r6c)
+        const EncGeo G = enc_geo(rl32(pwv, jj), rl32(szv, jj), rl32(rel, jj), lead);
+        emit_block256_g<true>(img, val, G, v, t);
         wave_lds_sync();
-        // the run's blocks are contiguous: whole 16-byte chunks, the chunk a
-        // block ends in carried into the next block's image (RunCopy)
-        rc.put(img, sb, dst, size, jj + 1u == R.n, t);
+        rc.put(img, G.c, (flush >> jj) & 1u, lead, trash_at, t);
         wave_lds_sync();
-        // only [0, sb + size) can be non-zero: clear it for the next block
-        zero_image(img, min((sb + size + 15u) >> 4, kImgU32 / 4u), t);
+        zero_image_n(img, G.c.n16, t); // only [0, sb + size) can be non-zero
         wave_lds_sync();
     });
-    (void)cap_end; // the batch entry points require out_cap >= the bound: no chunk passes the stream's end
+    rc.flush_tail(rel_end, lead, t);
 }
 
 // ---- two-pass encoder (plan -> run scan -> write): the production path ---
@@ -274,8 +293,7 @@ __global__ __launch_bounds__(256) void k_enc256v32_write(const uint32_t * __rest
         run_offsets(off, R.first, R.n, run_base(run_pre, run_tile, R.first / RUN), t, ov, ev);
         const uint32_t szv = static_cast<uint32_t>(ev - ov);
         const uint32_t pwv = t < R.n ? plan[R.first + t] : 0u;
-        write_run<D1, PROBE>(R, in, starts, start0, szv, pwv, static_cast<uint32_t>(ov), static_cast<uint32_t>(ov >> 32), img,
-                             val_all[wv], out_base, out_base + out_cap, t);
+        write_run<D1, PROBE>(R, in, starts, start0, szv, pwv, ov, img, val_all[wv], out_base, out_base + out_cap, t);
     }
 }
 

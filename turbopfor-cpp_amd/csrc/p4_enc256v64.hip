@@ -11,7 +11,7 @@
 // Each block is built in its own LDS image whose dword phase puts the base
 // payload on a dword (a 256v64 unit's second block starts at an arbitrary
 // byte), then copied out in whole 16-byte chunks, the chunk a block ends in
-// carried into the next block of the run (RunCopy, p4_enc32.h).
+// carried into the next block of the run (RunCopyB, p4_enc32.h).
 #include "p4_scan.h"
 
 #include "p4_generic.h"
@@ -27,6 +27,11 @@ constexpr uint32_t kVal64U32 = 128;   // staged low halves (b <= 32 base packing
 constexpr int kEnc64PolPlan = 2;      // plan pass value loads: nontemporal (+1.5-3%, r5s)
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t rl32w64(uint32_t v, uint32_t lane)
+{
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(lane)));
+}
 
 struct Chunk64
 {
@@ -54,17 +59,6 @@ __device__ __forceinline__ void delta_encode64(uint64_t & x0, uint64_t & x1, uin
 
 // Plan word of one block: b | bx << 7 | xn << 14 | raw << 22 (23 bits).
 __device__ __forceinline__ uint32_t plan64_word(const PlanG & P) { return P.b | (P.bx << 7) | (P.xn << 14) | (P.raw << 22); }
-
-__device__ __forceinline__ PlanG plan64_unword(uint32_t w, uint32_t size)
-{
-    PlanG P;
-    P.b = w & 0x7Fu;
-    P.bx = (w >> 7) & 0x7Fu;
-    P.xn = (w >> 14) & 0xFFu;
-    P.raw = (w >> 22) & 1u;
-    P.size = size;
-    return P;
-}
 
 __device__ __forceinline__ PlanG plan_block128v64(uint64_t x0, uint64_t x1, uint32_t * hist, uint32_t t)
 {
@@ -95,47 +89,85 @@ __device__ __forceinline__ void or_pair64(uint32_t * img, uint32_t bit, uint64_t
             atomicOr(&img[q + i], w[i]);
 }
 
+// or_pair64 with the store count decided by nested wave-uniform tests of nb
+// ((62 + 2 nb) >> 5 dwords at most; round 6: the unrolled `i < maxw` bound
+// compiled into four compares per call)
+__device__ __forceinline__ void or_pair64n(uint32_t * img, uint32_t bit, uint64_t a, uint64_t b, uint32_t nb)
+{
+    const uint64_t lo = a | ((b << (nb - 1u)) << 1);
+    const uint64_t hi = b >> (64u - nb);
+    const uint32_t sh = bit & 31u, q = bit >> 5;
+    atomicOr(&img[q], static_cast<uint32_t>(lo) << sh);
+    atomicOr(&img[q + 1u], static_cast<uint32_t>((lo << sh) >> 32));
+    if (nb > 1u)
+    {
+        atomicOr(&img[q + 2u], static_cast<uint32_t>((((hi << 32) | (lo >> 32)) << sh) >> 32));
+        if (nb > 17u)
+        {
+            atomicOr(&img[q + 3u], static_cast<uint32_t>((hi << sh) >> 32));
+            if (nb > 33u)
+                atomicOr(&img[q + 4u], static_cast<uint32_t>(((hi >> 32) << sh) >> 32));
+        }
+    }
+}
+
+// Layout of one 128v64 block from its plan word (plan64_word), size, output
+// byte rel (relative to the run's 16-byte aligned output base) and the run's
+// lead (round 6, as enc_geo in p4_enc32.h): bh = the header's width (64 is
+// stored as 63), sb / pw = image byte of the block / dword of its base
+// payload, hdr = header bytes 0 | 1 << 8, v0 = the vbyte area.
+struct EncGeo64
+{
+    uint32_t b, bh, bx, xn, raw, sb, pw, hdr, v0;
+    CopyGeo c;
+};
+
+__device__ __forceinline__ EncGeo64 enc_geo64(uint32_t w, uint32_t size, uint32_t rel, uint32_t lead)
+{
+    EncGeo64 G;
+    G.b = w & 0x7Fu;
+    G.bx = (w >> 7) & 0x7Fu;
+    G.xn = (w >> 14) & 0xFFu;
+    G.raw = (w >> 22) & 1u;
+    G.bh = G.b >= 64u ? 63u : G.b;
+    const bool bmp = G.bx != 0u && G.bx <= 64u, cst = G.bx == 66u;
+    const uint32_t xbytes = bmp ? ((G.xn * G.bx + 7u) >> 3) : 0u;
+    const uint32_t po = G.bx == 0u ? 1u : (bmp ? 18u + xbytes : 2u); // payload offset in the block
+    G.sb = cst ? kImgLead : kImgLead + ((4u - (po & 3u)) & 3u);
+    G.pw = (G.sb + po) >> 2;
+    G.hdr = G.bx == 0u ? G.bh : (bmp ? ((0x80u | G.bh) | (G.bx << 8)) : (cst ? (0xC0u | G.bh) : ((0x40u | G.bh) | (G.xn << 8))));
+    G.v0 = G.sb + 2u + 16u * G.b;
+    G.c = copy_geo(G.sb, size, rel, lead, kImg64U32);
+    return G;
+}
+
 // Build one 128v64 block (p4Enc128v64 = writeHeader64 + p4Enc128v64Payload)
-// in the zeroed image; returns sb, the image byte of the block's first byte.
-__device__ __forceinline__ uint32_t emit_block128v64(uint32_t * img, uint32_t * val, const PlanG & P, uint64_t x0, uint64_t x1,
-                                                     uint32_t t)
+// in the zeroed image from its layout G.  Round 6: the header, constant,
+// bitmap and raw-marker bytes are stored from every lane (unowned lanes to
+// their scratch bytes), not in single-lane exec-mask sections.
+__device__ __forceinline__ void emit_block128v64_g(uint32_t * img, uint32_t * val, const EncGeo64 & G, uint64_t x0, uint64_t x1,
+                                                   uint32_t t)
 {
     uint8_t * const ib = reinterpret_cast<uint8_t *>(img);
-    const uint32_t b = P.b;
-    const uint32_t bh = b >= 64u ? 63u : b; // header stores 64 as 63
-    if (P.bx == 66u)
+    const uint32_t b = G.b;
+    const uint32_t trash_at = static_cast<uint32_t>(reinterpret_cast<uint8_t *>(val + 2u * t) - ib);
+    auto put = [&](bool own, uint32_t at, uint32_t k, uint32_t byte) {
+        ib[__builtin_unpredictable(own) ? at : trash_at + (k & 7u)] = static_cast<uint8_t>(byte);
+    };
+    if (G.bx == 66u)
     {
-        // constant block: ceil(b/8) bytes of element 0
+        // constant block: header, ceil(b/8) bytes of element 0
         const uint64_t c = readlane_u64(x0, 0) & mask64d(b);
-        if (t == 0)
-            ib[kImgLead] = static_cast<uint8_t>(0xC0u | bh);
-        if (t < ((b + 7u) >> 3))
-            ib[kImgLead + 1u + t] = static_cast<uint8_t>(c >> (8u * t));
-        return kImgLead;
+        put(t <= ((b + 7u) >> 3), kImgLead + t, 0u, t == 0u ? G.hdr : static_cast<uint32_t>(c >> (8u * ((t - 1u) & 7u))));
+        return;
     }
+    const uint32_t sb = G.sb, pw = G.pw;
     const uint64_t m = mask64d(b);
-    const uint32_t xbytes = (P.bx != 0u && P.bx <= 64u) ? ((P.xn * P.bx + 7u) >> 3) : 0u;
-    const uint32_t po = P.bx == 0u ? 1u : (P.bx <= 64u ? 18u + xbytes : 2u); // payload offset in the block
-    const uint32_t sb = kImgLead + ((4u - (po & 3u)) & 3u);
-    const uint32_t pw = (sb + po) >> 2;
     const uint64_t m0 = x0 & m, m1 = x1 & m;
     const uint32_t f0 = x0 > m, f1 = x1 > m;
-    // headers
-    if (t == 0)
-    {
-        if (P.bx == 0u)
-            ib[sb] = static_cast<uint8_t>(bh);
-        else if (P.bx <= 64u)
-        {
-            ib[sb] = static_cast<uint8_t>(0x80u | bh);
-            ib[sb + 1u] = static_cast<uint8_t>(P.bx);
-        }
-        else
-        {
-            ib[sb] = static_cast<uint8_t>(0x40u | bh);
-            ib[sb + 1u] = static_cast<uint8_t>(P.xn);
-        }
-    }
+    // header bytes 0 and 1 from lanes 0 and 1 (a plain block's byte 1 is a
+    // payload byte: 0 here, OR-ed below)
+    put(t < 2u, sb + t, 0u, G.hdr >> (8u * (t & 1u)));
     // base payload (bitpack128v64Scalar, bitpack128v64_scalar.cpp:38-104)
     if (b != 0u && b <= 32u)
     {
@@ -151,53 +183,42 @@ __device__ __forceinline__ uint32_t emit_block128v64(uint32_t * img, uint32_t * 
 #pragma unroll
             for (uint32_t i = 0; i < 4; ++i)
                 x[i] = val[(4u * (4u * r + i) + l) ^ 2u];
-            or_run(img, pw + l, 4u, 4u * r * b, x, 4u, b, run_maxw(4u, b));
+            or_run4(img, pw + l, 4u, 4u * r * b, x, b);
         }
+        wave_lds_sync(); // val is scratch below
     }
     else if (b > 32u)
     {
         // horizontal 64-bit stream: values 2t, 2t+1 are consecutive
-        or_pair64(img, pw * 32u + 2u * t * b, m0, m1, b);
+        or_pair64n(img, pw * 32u + 2u * t * b, m0, m1, b);
     }
-    if (P.bx == 0u)
-        return sb;
+    if (G.bx == 0u)
+        return;
     const uint64_t B0 = __ballot(f0), B1 = __ballot(f1);
     const uint32_t cnt = f0 + f1;
     const uint32_t before = static_cast<uint32_t>(__builtin_popcountll(B0 & lanemask_lt()) + __builtin_popcountll(B1 & lanemask_lt()));
     const uint64_t e0 = b >= 64u ? 0ull : (x0 >> b), e1 = b >= 64u ? 0ull : (x1 >> b);
-    // Exception bytes go out as plain byte stores from every lane in every
-    // step: bytes a lane does not own go to its own 8 scratch bytes in `val`
-    // (free once the base payload is packed), so the steps carry no
-    // exec-mask sections (round 4, as emit_block256).
-    const uint32_t trash_at = static_cast<uint32_t>(reinterpret_cast<uint8_t *>(val + 2u * t) - ib);
-    auto put = [&](bool own, uint32_t at, uint32_t k, uint32_t byte) {
-        ib[__builtin_unpredictable(own) ? at : trash_at + (k & 7u)] = static_cast<uint8_t>(byte);
-    };
-    if (P.bx <= 64u)
+    if (G.bx <= 64u)
     {
         // [0x80|b][bx][bitmap 16 B][xn * bx bits][base]: bitmap byte k holds
         // elements 8k..8k+7, i.e. lanes 4k..4k+3 (x0 on even bits, x1 on odd)
-        if (t < 16u)
-        {
-            uint32_t n0 = static_cast<uint32_t>(B0 >> (4u * t)) & 15u, n1 = static_cast<uint32_t>(B1 >> (4u * t)) & 15u;
-            n0 = (n0 | (n0 << 2)) & 0x33u;
-            n0 = (n0 | (n0 << 1)) & 0x55u;
-            n1 = (n1 | (n1 << 2)) & 0x33u;
-            n1 = (n1 | (n1 << 1)) & 0x55u;
-            ib[sb + 2u + t] = static_cast<uint8_t>(n0 | (n1 << 1));
-        }
-        const uint64_t mx = mask64d(P.bx);
+        const uint32_t k = t & 15u;
+        uint32_t n0 = static_cast<uint32_t>(B0 >> (4u * k)) & 15u, n1 = static_cast<uint32_t>(B1 >> (4u * k)) & 15u;
+        n0 = (n0 | (n0 << 2)) & 0x33u;
+        n0 = (n0 | (n0 << 1)) & 0x55u;
+        n1 = (n1 | (n1 << 2)) & 0x33u;
+        n1 = (n1 | (n1 << 1)) & 0x55u;
+        put(t < 16u, sb + 2u + k, 0u, n0 | (n1 << 1));
+        const uint64_t mx = mask64d(G.bx);
         if (cnt != 0u) // lanes without exceptions share `before` with a neighbour: no zero ORs
-            or_pair64(img, (sb + 18u) * 8u + before * P.bx, (f0 ? e0 : e1) & mx, cnt > 1u ? (e1 & mx) : 0ull, P.bx);
-        return sb;
+            or_pair64n(img, (sb + 18u) * 8u + before * G.bx, (f0 ? e0 : e1) & mx, cnt > 1u ? (e1 & mx) : 0ull, G.bx);
+        return;
     }
     // vbyte: [0x40|b][xn][base 16b][V][positions]
-    const uint32_t v0 = sb + 2u + 16u * b;
-    if (P.raw)
+    const uint32_t v0 = G.v0;
+    if (G.raw)
     {
         // 0xFF, xn raw LE u64, xn position bytes
-        if (t == 0)
-            ib[v0] = 0xFFu;
         const uint32_t a0 = v0 + 1u + 8u * before, a1 = a0 + 8u * f0;
 #pragma unroll
         for (uint32_t k = 0; k < 8u; ++k)
@@ -205,10 +226,11 @@ __device__ __forceinline__ uint32_t emit_block128v64(uint32_t * img, uint32_t * 
             put(f0, a0 + k, k, static_cast<uint32_t>(e0 >> (8u * k)));
             put(f1, a1 + k, k, static_cast<uint32_t>(e1 >> (8u * k)));
         }
-        const uint32_t pp = v0 + 1u + 8u * P.xn + before;
+        const uint32_t pp = v0 + 1u + 8u * G.xn + before;
         put(f0, pp, 0u, 2u * t);
         put(f1, pp + f0, 1u, 2u * t + 1u);
-        return sb;
+        put(t == 0u, v0, 2u, 0xFFu);
+        return;
     }
     // vbPut64 (p4_scalar_internal.cpp:447-476): marker byte, then up to 8 bytes
     const uint32_t l0 = f0 ? vblen64(e0) : 0u, l1 = f1 ? vblen64(e1) : 0u;
@@ -231,7 +253,6 @@ __device__ __forceinline__ uint32_t emit_block128v64(uint32_t * img, uint32_t * 
     vbput(f1, pos + l0, e1, l1);
     put(f0, v0 + vtot + before, 0u, 2u * t);
     put(f1, v0 + vtot + before + f0, 1u, 2u * t + 1u);
-    return sb;
 }
 
 // A wave's run of up to kEnc64Run consecutive units (NB blocks of 128 u64);
@@ -369,33 +390,45 @@ __global__ __launch_bounds__(256) void k_enc128v64_write(const uint64_t * __rest
     const uint64_t stv = D1 ? R.start_lane(in, starts, start0, t) : 0ull;
     uint64_t ov, ev;
     run_offsets(off, R.first, R.n, run_base(run_pre, run_tile, R.first / kEnc64Run), t, ov, ev);
+    const uint32_t szv = static_cast<uint32_t>(ev - ov);
     const uint64_t pwv = t < R.n ? plan[R.first + t] : 0ull;
     const uint64_t out_base = reinterpret_cast<uint64_t>(out);
     (void)out_cap; // tpf_enc_batch requires out_cap >= tpf_enc_bound: no chunk passes the stream's end
     zero_image(img, kImg64U32 / 4u, t);
     wave_lds_sync();
-    RunCopy rc; // the run's blocks are contiguous: whole 16-byte chunks (p4_enc32.h)
+    // the run's output through one descriptor based at its first byte rounded
+    // down to 16, 32-bit offsets (RunCopyB, p4_enc32.h; round 6)
+    const uint64_t ab = out_base + ov;
+    const uint64_t A = readlane_u64(ab, 0) & ~15ull;
+    const uint32_t rel = static_cast<uint32_t>(ab - A);
+    const uint32_t lead = rl32w64(rel, 0); // < 16
+    const uint32_t rel_end = rl32w64(rel + szv, R.n - 1u);
+    RunCopyB rc;
+    rc.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(A), static_cast<short>(0), static_cast<int>(rel_end), 0x00020000);
+    uint32_t * const val = val_all[wv];
+    const uint32_t trash_at = static_cast<uint32_t>(reinterpret_cast<uint8_t *>(val + 2u * t) - reinterpret_cast<uint8_t *>(img));
     R.walk(t, [&](const Chunk64 & c, uint32_t jj) {
         uint64_t x[2][2];
         unit_values<NB, D1>(c, D1 ? readlane_u64(stv, jj) : 0ull, t, x);
-        const uint64_t o = readlane_u64(ov, jj);
-        const uint32_t usize = static_cast<uint32_t>(readlane_u64(ev, jj) - o);
+        const uint32_t urel = rl32w64(rel, jj), usize = rl32w64(szv, jj);
         const uint64_t w = readlane_u64(pwv, jj);
         const uint32_t size0 = NB == 2 ? static_cast<uint32_t>(w >> 46) : usize;
 #pragma unroll
         for (uint32_t u = 0; u < NB; ++u)
         {
             const uint32_t size = u == 0 ? size0 : usize - size0;
-            const PlanG P = plan64_unword(static_cast<uint32_t>(w >> (23u * u)) & 0x7FFFFFu, size);
-            const uint64_t dst = out_base + o + (u == 0 ? 0u : size0);
-            const uint32_t sb = emit_block128v64(img, val_all[wv], P, x[u][0], x[u][1], t);
+            const uint32_t brel = urel + (u == 0 ? 0u : size0);
+            const EncGeo64 G = enc_geo64(static_cast<uint32_t>(w >> (23u * u)) & 0x7FFFFFu, size, brel, lead);
+            emit_block128v64_g(img, val, G, x[u][0], x[u][1], t);
             wave_lds_sync();
-            rc.put(img, sb, dst, size, u + 1u == NB && jj + 1u == R.n, t);
+            // the block that completes the run's partial first chunk stores its bytes [lead, 16)
+            rc.put(img, G.c, lead != 0u && brel < 16u && brel + size >= 16u, lead, trash_at, t);
             wave_lds_sync();
-            zero_image(img, min((sb + size + 15u) >> 4, kImg64U32 / 4u), t);
+            zero_image_n(img, G.c.n16, t); // only [0, sb + size) can be non-zero
             wave_lds_sync();
         }
     });
+    rc.flush_tail(rel_end, lead, t);
 }
 
 } // namespace tpf::dev

@@ -521,67 +521,354 @@ __device__ __forceinline__ void copy_out_image16(const uint32_t * img, uint32_t 
 }
 
 
-// Copy-out of a wave's RUN of consecutive blocks (round 5): the blocks of a
-// run are contiguous in the output, so the 16-byte output chunk a block ends
-// in is completed by the next block of the same wave.  The wave carries the
-// chunk's bytes produced so far (lane t < 16 holds byte t) and places them in
-// the next block's image just before its first byte, so every chunk is
-// stored whole with one 16-byte store -- the per-block byte-store edges of
-// copy_out_image16 (head and tail chunks written by 32 lanes byte by byte,
-// every block) disappear.  Only the run's first chunk (its first `lead`
-// bytes belong to the previous run's wave) and its last chunk are partial,
-// written with byte stores.  Needs out_cap >= the stream's size (the batch
-// entry points check the bound), sb >= 16 (kImgLead) and a zeroed image in
-// front of the block.
-struct RunCopy
-{
-    uint32_t carry = 0u; // lane t < (next dst & 15): byte t of the open output chunk
-    uint32_t lead = 0u;  // bytes at the start of the open chunk that are not this run's
-    bool fresh = true;   // no block copied yet
+// Round 5's RunCopy (a run's blocks copied out in whole 16-byte chunks, the
+// open chunk carried from block to block through lanes 0-15) became RunCopyB
+// below in round 6: the same chunking, addressed through one buffer
+// descriptor per run with the layout read per block.
 
-    // Block of `size` bytes at image byte sb, destined for dst; last: the
-    // run's last block (flush the open chunk).
-    __device__ __forceinline__ void put(uint32_t * img, uint32_t sb, uint64_t dst, uint32_t size, bool last, uint32_t t)
+// ---- round 6: the write pass's control plane in lanes ------------------------
+// the D1 write pass issued 136 SALU + 29 branches per block
+// against 141 VALU.  A CU has one scalar unit for its four SIMDs (a wave64
+// VALU takes 2 cycles on one SIMD-32), so the scalar side bound the pass:
+// every block re-derived its layout (payload offset, image phase, header
+// bytes, copy-out chunk range, 64-bit destination) with scalar arithmetic
+// and wrapped each single-lane step in exec-mask sections.  As the decoder's
+// RunPlaneT (p4_dec_run.h) did for decoding, the layout of every block of a
+// wave run is now computed ONCE per run in vector lanes (lane j = block j)
+// and read per block with v_readlane; single-lane stores become stores from
+// every lane with unowned lanes sent to their own trash dword (LDS) or an
+// out-of-range buffer offset (HBM: the store is dropped), so they need no
+// exec mask; and the copy-out addresses the run's output through one buffer
+// descriptor with 32-bit offsets.
+
+// Buffer offset that the hardware range check drops (stores) / zeroes (loads).
+constexpr uint32_t kOob = 0x80000000u;
+// dwords of a write-pass block image (256v32 and 128v64: 4..7 lead bytes + a
+// block of <= 2276 B + slack, a 16-byte multiple)
+constexpr uint32_t kImgU32Max = 592;
+
+// Copy-out layout of a block built at image byte sb (RunCopyB), from its
+// size, its output byte rel relative to the run's 16-byte aligned output base
+// and the run's lead (= the first block's rel: bytes of the open chunk that
+// belong to the previous run).  ph: bytes of the open chunk before the block;
+// base: image byte of that chunk; a16: its output offset; nfull: chunks the
+// block completes; r: bytes of the chunk it leaves open (at image byte tb);
+// kfirst: 1 when chunk 0 is the run's partial first chunk (byte stores);
+// n16: image chunks to clear after the block.
+struct CopyGeo
+{
+    uint32_t ph, base, a16, nfull, r, tb, kfirst, n16;
+};
+
+__device__ __forceinline__ CopyGeo copy_geo(uint32_t sb, uint32_t size, uint32_t rel, uint32_t lead, uint32_t img_u32)
+{
+    CopyGeo C;
+    C.ph = rel & 15u;
+    C.base = sb - C.ph;
+    const uint32_t end = C.ph + size;
+    C.nfull = end >> 4;
+    C.r = end & 15u;
+    C.tb = C.base + 16u * C.nfull;
+    C.a16 = rel & ~15u;
+    C.kfirst = (lead != 0u && rel < 16u) ? 1u : 0u;
+    C.n16 = min((sb + size + 15u) >> 4, img_u32 / 4u);
+    return C;
+}
+
+// Layout of one block.  sb: image byte of the block's first byte; pw: image
+// dword of its base payload; hdr: header bytes 0 | 1 << 8 (byte 1 is 0 for a
+// plain block: a payload byte, OR-ed afterwards); v0 / pbase: vbyte area /
+// position bytes; c: copy-out.
+struct EncGeo
+{
+    uint32_t b, m, bx, xn, raw, sb, pw, hdr, v0, pbase;
+    CopyGeo c;
+};
+
+// Lane form: pwd = plan word (b | bx << 8 | xn << 16 | raw << 25), size =
+// block bytes, rel = its output byte relative to the run's 16-byte aligned
+// output base, lead = the run's first rel (bytes of the open chunk that
+// belong to the previous run).
+__device__ __forceinline__ EncGeo enc_geo(uint32_t pwd, uint32_t size, uint32_t rel, uint32_t lead)
+{
+    EncGeo G;
+    G.b = pwd & 0xFFu;
+    G.bx = (pwd >> 8) & 0xFFu;
+    G.xn = (pwd >> 16) & 0x1FFu;
+    G.raw = (pwd >> 25) & 1u;
+    G.m = mask32(G.b);
+    const bool bmp = G.bx != 0u && G.bx <= 32u, cst = G.bx == 34u;
+    const uint32_t xbytes = bmp ? ((G.xn * G.bx + 7u) >> 3) : 0u;
+    const uint32_t po = G.bx == 0u ? 1u : (bmp ? 34u + xbytes : 2u); // payload offset in the block
+    G.sb = cst ? kImgLead : kImgLead + ((4u - (po & 3u)) & 3u);
+    G.pw = (G.sb + po) >> 2;
+    G.hdr = G.bx == 0u ? G.b : (bmp ? ((0x80u | G.b) | (G.bx << 8)) : (cst ? (0xC0u | G.b) : ((0x40u | G.b) | (G.xn << 8))));
+    G.v0 = G.sb + 2u + 32u * G.b;
+    G.pbase = G.sb + size - G.xn;
+    G.c = copy_geo(G.sb, size, rel, lead, kImgU32Max);
+    return G;
+}
+
+// OR a run of four nb-bit values (or_run's packing) with the store count
+// decided by nested wave-uniform tests: a block of width <= 8 pays one test
+// (or_run's unrolled `i < maxw` bound compiled into three compares).
+__device__ __forceinline__ void or_run4(uint32_t * img, uint32_t dw0, uint32_t stride, uint32_t bit, const uint32_t x[4], uint32_t nb)
+{
+    const uint32_t sh = bit & 31u, q = bit >> 5;
+    const uint64_t a = static_cast<uint64_t>(x[0]) | (static_cast<uint64_t>(x[1]) << nb);
+    const uint64_t c = static_cast<uint64_t>(x[2]) | (static_cast<uint64_t>(x[3]) << nb);
+    const uint32_t n2 = 2u * nb;
+    const uint64_t lo = a | ((c << (n2 - 1u)) << 1);
+    const uint64_t hi = c >> (64u - n2);
+    const uint32_t d1 = static_cast<uint32_t>(lo >> 32), d2 = static_cast<uint32_t>(hi);
+    atomicOr(&img[dw0 + stride * q], static_cast<uint32_t>(lo) << sh);
+    atomicOr(&img[dw0 + stride * (q + 1u)], static_cast<uint32_t>((lo << sh) >> 32));
+    if (nb > 8u) // (31 + 4 nb + 31) >> 5 dwords at most
     {
-        typedef __attribute__((address_space(1))) uint8_t gu8;
-        typedef __attribute__((address_space(1))) u32x4 gu32x4;
-        uint8_t * ib = reinterpret_cast<uint8_t *>(img);
-        const uint32_t ph = static_cast<uint32_t>(dst & 15u); // bytes of the open chunk already produced
-        if (fresh)
+        atomicOr(&img[dw0 + stride * (q + 2u)], static_cast<uint32_t>((((static_cast<uint64_t>(d2) << 32) | d1) << sh) >> 32));
+        if (nb > 16u)
         {
-            lead = ph;
-            fresh = false;
+            atomicOr(&img[dw0 + stride * (q + 3u)], static_cast<uint32_t>((hi << sh) >> 32));
+            if (nb > 24u)
+                atomicOr(&img[dw0 + stride * (q + 4u)], static_cast<uint32_t>(((hi >> 32) << sh) >> 32));
         }
-        const uint32_t base = sb - ph; // image byte of the open chunk's byte 0
-        // the carried bytes in front of the block (lanes t < lead carry zeros: not stored)
-        if (t < ph)
-            ib[base + t] = static_cast<uint8_t>(carry);
+    }
+}
+
+template <bool PAD>
+__device__ __forceinline__ void pack_base_runs4(uint32_t * img, uint32_t pw, const uint32_t * val, uint32_t b, uint32_t t)
+{
+    if (b == 0u)
+        return;
+    const uint32_t l = t >> 3, r = t & 7u;
+    const uint32_t e = val_idx<PAD>(32u * r + l); // element of group 4r in column l
+    const uint32_t x[4] = {val[e], val[e + 8u], val[e + 16u], val[e + 24u]};
+    if (b <= 8u)
+    {
+        // the run's 4b <= 32 bits in one dword, placed by one 64-bit shift
+        // (or_run4 builds two 64-bit pairs: ~9 VALU more per block; C3's
+        // posting blocks have b <= 8)
+        const uint32_t run = x[0] | (x[1] << b) | (x[2] << (2u * b)) | (x[3] << (3u * b));
+        const uint32_t bit = 4u * r * b, q = bit >> 5;
+        const uint64_t w = static_cast<uint64_t>(run) << (bit & 31u);
+        atomicOr(&img[pw + l + 8u * q], static_cast<uint32_t>(w));
+        atomicOr(&img[pw + l + 8u * (q + 1u)], static_cast<uint32_t>(w >> 32));
+        return;
+    }
+    or_run4(img, pw + l, 8u, 4u * r * b, x, b);
+}
+
+// Build a block image from its uniform layout G (emit_block256's bytes:
+// p4enc256v32_scalar.cpp:49-194, vbEnc32 p4_scalar_internal.cpp:47-89,
+// :163-197), with no exec-mask section on the plain and vbyte paths.
+template <bool PAD>
+__device__ __forceinline__ void emit_block256_g(uint32_t * img, uint32_t * val, const EncGeo & G, const u32x4 & v, uint32_t t)
+{
+    uint8_t * const ib = reinterpret_cast<uint8_t *>(img);
+    uint32_t * const trash = val + kEncTrash + t;
+    const uint32_t trash_at = static_cast<uint32_t>(reinterpret_cast<uint8_t *>(trash) - ib); // (mod 2^32: LDS addresses are 32-bit)
+    auto put = [&](bool own, uint32_t at, uint32_t byte) {
+        ib[__builtin_unpredictable(own) ? at : trash_at] = static_cast<uint8_t>(byte);
+    };
+    const uint32_t b = G.b;
+    if (G.bx == 34u)
+    {
+        // constant block (p4enc256v32_scalar.cpp:183-190): header, ceil(b/8) value bytes
+        const uint32_t x = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v.x), 0)) & G.m;
+        put(t <= ((b + 7u) >> 3), kImgLead + t, t == 0u ? G.hdr : x >> (8u * ((t - 1u) & 3u)));
+        return;
+    }
+    // header bytes 0 and 1 from lanes 0 and 1 (a plain block's byte 1 is a
+    // payload byte: 0 here, OR-ed below; the wave's LDS operations run in order)
+    put(t < 2u, G.sb + t, G.hdr >> (8u * (t & 1u)));
+    const uint32_t m = G.m;
+    *reinterpret_cast<u32x4 *>(val + val_idx<PAD>(4u * t)) = u32x4{v.x & m, v.y & m, v.z & m, v.w & m};
+    if (G.bx == 0u)
+    {
         wave_lds_sync();
-        gu8 * const a16 = (gu8 *)(dst & ~15ull);
-        const uint32_t end = ph + size;
-        const uint32_t nfull = end >> 4; // chunks completed by this block
-        const uint32_t k0 = lead != 0u ? 1u : 0u;
-        const uint32_t bs = base & 3u;
-        for (uint32_t k = k0 + t; k < nfull; k += 64u)
+        pack_base_runs4<PAD>(img, G.pw, val, b, t);
+        return;
+    }
+    const uint32_t f0 = v.x > m, f1 = v.y > m, f2 = v.z > m, f3 = v.w > m;
+    const uint32_t my = f0 | (f1 << 1) | (f2 << 2) | (f3 << 3);
+    const uint32_t cnt = f0 + f1 + f2 + f3;
+    const uint32_t before = wave_incl_scan(cnt) - cnt; // exceptions in elements < 4t
+    const uint32_t sh = b & 31u;
+    const uint32_t ex[4] = {v.x >> sh, v.y >> sh, v.z >> sh, v.w >> sh};
+    if (G.bx <= 32u)
+    {
+        // [0x80|b][bx][bitmap 32B][xn*bx bits horizontal][256v32 base]
+        const uint32_t mynext = wave_shl1(my, 0u);
+        put((t & 1u) == 0u, G.sb + 2u + (t >> 1), my | (mynext << 4));
+        wave_lds_sync();
+        pack_base_runs4<PAD>(img, G.pw, val, b, t);
+        uint32_t xr[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int j = 3; j >= 0; --j)
         {
-            const uint32_t q = (base >> 2) + 4u * k;
+            const bool fj = (my >> j) & 1u;
+            xr[3] = fj ? xr[2] : xr[3];
+            xr[2] = fj ? xr[1] : xr[2];
+            xr[1] = fj ? xr[0] : xr[1];
+            xr[0] = fj ? ex[j] : xr[0];
+        }
+        if (cnt != 0u) // lanes without exceptions share `before` with a neighbour: no zero ORs
+            or_run4(img, 0u, 1u, (G.sb + 34u) * 8u + before * G.bx, xr, G.bx);
+        return;
+    }
+    // vbyte: [0x40|b][xn][256v32 base][V][positions] -- emit_block256's two
+    // steps (position bytes by rank, then one rank per lane)
+    wave_lds_sync();
+    pack_base_runs4<PAD>(img, G.pw, val, b, t);
+    const uint32_t xn = G.xn, pbase = G.pbase, v0 = G.v0;
+    *reinterpret_cast<u32x4 *>(val + 4u * t) = u32x4{ex[0], ex[1], ex[2], ex[3]};
+    // the lane's i-th flagged element writes its position byte to rank
+    // before + i: i = 0 from every lane, i >= 1 only when a lane holds that
+    // many (two wave-uniform tests instead of a four-step maximum)
+    uint32_t rem = my;
+    auto scat = [&](uint32_t i) {
+        const bool on = rem != 0u;
+        const uint32_t j = on ? static_cast<uint32_t>(__builtin_ctz(rem)) : 0u;
+        rem &= rem - 1u;
+        put(on, pbase + before + i, 4u * t + j);
+    };
+    scat(0u);
+    if (__builtin_amdgcn_ballot_w64(cnt >= 2u) != 0ull)
+    {
+        scat(1u);
+        if (__builtin_amdgcn_ballot_w64(cnt >= 3u) != 0ull)
+        {
+            scat(2u);
+            scat(3u);
+        }
+    }
+    wave_lds_sync();
+    auto rank_value = [&](uint32_t r) { return val[ib[pbase + min(r, xn - 1u)]]; };
+    if (G.raw)
+    {
+        // 0xFF, xn raw LE words, the positions
+        for (uint32_t c = 0; c < xn; c += 64u)
+        {
+            const uint32_t r = c + t;
+            const bool on = r < xn;
+            const uint32_t x = rank_value(r), A = v0 + 1u + 4u * r;
+            put(on, A, x);
+            put(on, A + 1u, x >> 8);
+            put(on, A + 2u, x >> 16);
+            put(on, A + 3u, x >> 24);
+        }
+        put(t == 0u, v0, 0xFFu); // after the words: lane 0's own bytes above went to [v0 + 1, v0 + 5)
+        return;
+    }
+    uint32_t vb = v0; // byte of the chunk's first vbyte
+    uint32_t c = 0;
+    do // xn >= 1: the first 64 ranks without a loop test
+    {
+        const uint32_t r = c + t;
+        const bool on = r < xn;
+        const uint32_t x = rank_value(r);
+        const uint32_t d2 = x - 156u;
+        const bool g1 = x >= 156u;
+        if (__builtin_amdgcn_ballot_w64(on && x >= 16540u) == 0ull)
+        {
+            // every value of the chunk takes 1 or 2 bytes (posting-list
+            // gaps): rank r's first byte is at vb + r + the 2-byte values
+            // before it -- a ballot and mbcnt, no wave scan (the ranks in use
+            // are a prefix of the lanes)
+            const uint64_t two = __builtin_amdgcn_ballot_w64(on && g1);
+            const uint32_t A = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(two >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(two), vb + t));
+            vb += min(xn - c, 64u) + static_cast<uint32_t>(__builtin_popcountll(two));
+            const uint32_t lo = __builtin_unpredictable(g1) ? (0x9Cu + (d2 >> 8)) | ((d2 & 0xFFu) << 8) : x;
+            put(on, A, lo);
+            put(on && g1, A + 1u, lo >> 8);
+        }
+        else
+        {
+            const uint32_t d3 = x - 16540u;
+            const bool g2 = x >= 16540u, g3 = x >= 2113692u, g4 = x > 0xFFFFFFu;
+            const uint32_t L = on ? 1u + g1 + g2 + g3 + g4 : 0u;
+            const uint32_t incl = wave_incl_scan(L);
+            const uint32_t A = vb + incl - L;
+            vb += __builtin_amdgcn_readlane(incl, 63);
+            const uint32_t c2 = (0x9Cu + (d2 >> 8)) | ((d2 & 0xFFu) << 8);
+            const uint32_t c3 = (0xDCu + (d3 >> 16)) | ((d3 & 0xFFFFu) << 8);
+            const uint32_t c45 = (g4 ? 0xFDu : 0xFCu) | (x << 8);
+            const uint32_t c23 = __builtin_unpredictable(g2) ? c3 : c2;
+            const uint32_t c25 = __builtin_unpredictable(g3) ? c45 : c23;
+            const uint32_t lo = __builtin_unpredictable(g1) ? c25 : x;
+            put(on, A, lo);
+            put(L > 1u, A + 1u, lo >> 8);
+            put(L > 2u, A + 2u, lo >> 16);
+            put(L > 3u, A + 3u, lo >> 24);
+            put(L > 4u, A + 4u, x >> 24);
+        }
+        c += 64u;
+    } while (c < xn);
+}
+
+// Clear image chunks [0, n16): one exec-masked store per lane, a loop only
+// for images past 1 KB.
+__device__ __forceinline__ void zero_image_n(uint32_t * img, uint32_t n16, uint32_t t)
+{
+    if (t < n16)
+        reinterpret_cast<u32x4 *>(img)[t] = u32x4{0u, 0u, 0u, 0u};
+    if (n16 > 64u)
+        for (uint32_t i = 64u + t; i < n16; i += 64u)
+            reinterpret_cast<u32x4 *>(img)[i] = u32x4{0u, 0u, 0u, 0u};
+}
+
+// RunCopy with the layout from a run plane: the run's output is addressed
+// through ONE buffer descriptor (base = the run's first output byte rounded
+// down to 16, 32-bit offsets), chunk stores from every lane (lanes past the
+// block's chunks get kOob and store nothing), the carried bytes placed from
+// every lane (unowned lanes write their trash dword).  The run's partial
+// first chunk (bytes [lead, 16) of chunk 0) is stored by the block that
+// completes it (a wave-uniform test of the run's flush mask) and the partial
+// last chunk once after the run (flush_tail).
+struct RunCopyB
+{
+    uint32_t carry = 0u; // lane t < r: byte t of the open output chunk
+    __amdgpu_buffer_rsrc_t rs;
+
+    __device__ __forceinline__ void put(uint32_t * img, const CopyGeo & G, bool flush_lead, uint32_t lead, uint32_t trash_at,
+                                       uint32_t t)
+    {
+        uint8_t * ib = reinterpret_cast<uint8_t *>(img);
+        // the carried bytes in front of the block (lanes t < lead carry zeros: never stored)
+        ib[t < G.ph ? G.base + t : trash_at] = static_cast<uint8_t>(carry);
+        wave_lds_sync();
+        const uint32_t bs = G.base & 3u;
+        for (uint32_t k0 = G.kfirst;; k0 += 64u)
+        {
+            const uint32_t k = k0 + t;
+            const uint32_t q = (G.base >> 2) + 4u * k;
             const uint32_t w0 = img[q], w1 = img[q + 1], w2 = img[q + 2], w3 = img[q + 3], w4 = img[q + 4];
             const u32x4 c = u32x4{__builtin_amdgcn_alignbyte(w1, w0, bs), __builtin_amdgcn_alignbyte(w2, w1, bs),
                                   __builtin_amdgcn_alignbyte(w3, w2, bs), __builtin_amdgcn_alignbyte(w4, w3, bs)};
-            *(gu32x4 *)(a16 + 16u * k) = c;
+            __builtin_amdgcn_raw_buffer_store_b128(c, rs, static_cast<int>(k < G.nfull ? G.a16 + 16u * k : kOob), 0, 0);
+            if (__builtin_expect(G.nfull <= k0 + 64u, 1)) // wave-uniform: chunks left?
+                break;
         }
-        if (k0 != 0u && nfull != 0u)
+        if (flush_lead)
         {
-            // the run's first chunk: bytes [lead, 16) are ours
-            if (t >= lead && t < 16u)
-                a16[t] = ib[base + t];
-            lead = 0u;
+            // the run's first chunk: bytes [lead, 16) are ours (G.a16 == 0 here)
+            const uint32_t byte = ib[G.base + (t & 15u)];
+            __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rs, static_cast<int>(t >= lead && t < 16u ? t : kOob), 0, 0);
         }
-        const uint32_t r = end & 15u;
-        const uint32_t tb = base + 16u * nfull; // image byte of the new open chunk
-        carry = t < r ? static_cast<uint32_t>(ib[tb + t]) : 0u;
-        if (last && r != 0u && t >= lead && t < r)
-            a16[16u * nfull + t] = static_cast<uint8_t>(carry);
+        const uint32_t nb = ib[G.tb + (t & 15u)];
+        carry = t < G.r ? nb : 0u;
+    }
+
+    // after the run's last block: its partial last chunk (rel_end = the
+    // run's end relative to the descriptor; the run's first chunk is shared
+    // with the previous run when the whole run ends inside it)
+    __device__ __forceinline__ void flush_tail(uint32_t rel_end, uint32_t lead, uint32_t t)
+    {
+        const uint32_t r = rel_end & 15u;
+        const uint32_t lo = rel_end < 16u ? lead : 0u;
+        __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(carry), rs,
+                                             static_cast<int>(t >= lo && t < r ? (rel_end & ~15u) + t : kOob), 0, 0);
     }
 };
 

@@ -303,21 +303,32 @@ __global__ __launch_bounds__(256) void k_block_server(ServerReq * rq, ServerAns 
             }
             continue;
         }
-        // leave together: once one wave of the launch quits (idle or told to
-        // stop) every other follows; the shared words are read every 256th
-        // poll (the stop word every 256th too: each read of it crosses PCIe
-        // in mode 2)
-        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        // leave together: once one wave of the launch quits (idle, past its
+        // lifetime, or told to stop) every other follows at its next poll.
+        // The quit word (device memory) and the lifetime are checked on every
+        // poll (round 6, ADVICE r5: checked every 256th, the launch's waves
+        // left over up to 256 poll intervals while the host kept posting to
+        // mailboxes whose waves had gone).  The idle test (last_active) and
+        // the host's stop word are read every 256th poll (each read of the
+        // stop word crosses PCIe in mode 2).
+        if (uni(ld_agent(&ctl->quit)) != 0u)
+            break;
+        bool leave = __builtin_amdgcn_s_memrealtime() - born > max_ticks;
         if ((polls & 255u) == 0u)
         {
-            const uint64_t la = __hip_atomic_load(&ctl->last_active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (uni(ld_agent(&ctl->quit)) != 0u || ((polls & 63u) == 0u && uni(ld_sys(&rq->stop)) != 0u) ||
-                now - uni64(la) > idle_ticks || now - born > max_ticks)
-            {
-                if (t == 0)
-                    __hip_atomic_store(&ctl->quit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
+            const uint64_t la = uni64(__hip_atomic_load(&ctl->last_active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            // the clock is read AFTER last_active: another workgroup may have
+            // published a later time between an earlier clock read and the
+            // load, and `now - la` would wrap to ~2^64 (a spurious
+            // idle exit of the whole server)
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            leave = leave || (la < now && now - la > idle_ticks) || uni(ld_sys(&rq->stop)) != 0u;
+        }
+        if (leave)
+        {
+            if (t == 0)
+                __hip_atomic_store(&ctl->quit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
         }
         __builtin_amdgcn_s_sleep(1);
     }
