@@ -4,7 +4,8 @@
 list chained from start0.
 usage: python scripts/enc_kernel_times.py [nblocks] [reps] [mode] [c4|c3]
 mode 0: the library's choice; 1/2: tpfm_enc256v32 pass probes (the plan /
-write pass with the coding removed, c4 only); 3 two-pass; 4 slot; 5 slot
+write pass with the coding removed; 1 c4 only, 2 also c3: after the real D1
+plan); 3 two-pass; 4 slot; 5 slot
 without the fused scans.  Prints HIP-event ms per launch."""
 import os
 import sys

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <latch>
 #include <thread>
 #include <vector>
 
@@ -66,8 +67,12 @@ int main(int argc, char ** argv)
         uint64_t launches[2] = {0, 0}; // block-server launches during each timed phase
         for (int phase = 0; phase < 2; ++phase) // 0 = encode, 1 = decode
         {
-            std::atomic<int> ready{0};
-            std::atomic<bool> go{false};
+            // blocking latches, not yield loops: on a machine whose CPU time is
+            // capped by a cgroup quota, T threads yield-spinning between their
+            // warm-up call and the start burn the quota, and the timed phase
+            // then runs throttled (round 6: the spread of the 48-128 thread
+            // numbers before this)
+            std::latch ready(T), go(1);
             std::vector<std::thread> th;
             std::vector<double> secs(T);
             for (int i = 0; i < T; ++i)
@@ -77,13 +82,11 @@ int main(int argc, char ** argv)
                     fill_block(v, static_cast<uint32_t>(i));
                     unsigned char * end = enc(v, buf); // warm: also relaunches the server
                     if (!end)
-                    {
                         bad++;
+                    ready.count_down();
+                    go.wait();
+                    if (!end)
                         return;
-                    }
-                    ready++;
-                    while (!go.load())
-                        std::this_thread::yield();
                     const auto t0 = std::chrono::steady_clock::now();
                     for (int k = 0; k < K; ++k)
                     {
@@ -99,11 +102,13 @@ int main(int argc, char ** argv)
                     if (phase == 1 && std::memcmp(out, v, 4u * (nv >= 256u ? 256u : nv)) != 0)
                         bad++;
                 });
-            while (ready.load() + bad.load() < T)
-                std::this_thread::yield();
+            ready.wait();
+            // let a cgroup quota period pass: the warm-up's CPU time (thread
+            // creation, T first calls) is not charged to the timed phase
+            std::this_thread::sleep_for(std::chrono::milliseconds(200));
             const uint64_t l0 = launches_now();
             const auto t0 = std::chrono::steady_clock::now();
-            go = true;
+            go.count_down();
             for (auto & t : th)
                 t.join();
             const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

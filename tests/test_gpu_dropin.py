@@ -291,8 +291,8 @@ def test_host_streams_of_two_threads_overlap():
 @pytest.mark.parametrize("nthreads", [16, 80, 128])
 def test_per_block_server_concurrent_threads(nthreads):
     """16 threads (each its own mailbox), 80 and 128 (more than the server's
-    64 mailboxes: callers are admitted through the mailbox semaphore and, with
-    more threads than CPUs, sleep while they wait) call at once: every thread's
+    64 mailboxes: callers wait for a free one and, with more threads than
+    CPUs, sleep while they wait) call at once: every thread's
     encode -> decode round trip of its own blocks is byte-exact (oracle),
     bit-exact, and every returned end pointer is right."""
     import threading

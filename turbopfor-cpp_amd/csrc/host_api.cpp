@@ -31,7 +31,6 @@
 #include <cstring>
 #include <fstream>
 #include <mutex>
-#include <semaphore>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -304,15 +303,12 @@ struct Server
     struct alignas(64) Box
     {
         std::atomic<uint32_t> busy{0};
-        std::atomic<uint32_t> reqno{0}; // last request number posted to this mailbox
+        std::atomic<uint32_t> reqno{0};   // last request number posted to this mailbox
+        std::atomic<uint32_t> waiters{0}; // callers blocked on `busy` (lease, crowded)
     };
     Box box[tpf::kServerBoxes];
     bool held = false; // every mailbox taken by the pause (pause thread only)
-    // With more calling threads than mailboxes, callers are admitted through
-    // this semaphore first (a futex wait, no CPU), so that at most one caller
-    // per mailbox searches the lock words: 128 threads scanning 64 lines
-    // between naps served 0.9M calls/s (r6b).
-    std::counting_semaphore<tpf::kServerBoxes> gate{tpf::kServerBoxes};
+
 
     static void * pinned(size_t bytes, void ** dev_view)
     {
@@ -418,7 +414,14 @@ struct Server
                box[i].busy.compare_exchange_strong(z, 1u, std::memory_order_seq_cst);
     }
     // A free mailbox, searched from a per-thread starting mailbox (up to 64
-    // threads get distinct ones); past 64 concurrent callers, wait by yielding.
+    // threads get distinct ones).  With more calling threads than CPUs a
+    // caller tries its own mailbox and three others a quarter of the ring
+    // apart, then blocks on its own mailbox's lock word until that mailbox is
+    // released (a futex wait: no CPU, no polling).  Round 6: a full pass over
+    // 64 lock words owned by other cores costs microseconds of CPU, and with
+    // 128 callers every waiting thread made such passes between naps (0.9M
+    // calls/s, r6b); a semaphore admitting 64 callers at a time paid a futex
+    // wake per call (0.75M, r6f); napping waiters paid a wake-up per nap (r6g).
     int lease()
     {
         thread_local const uint32_t hint = [] {
@@ -427,20 +430,31 @@ struct Server
         }();
         for (;;)
         {
-            for (uint32_t k = 0; k < tpf::kServerBoxes; ++k)
+            const bool crowd = crowded();
+            const uint32_t tries = crowd ? 4u : tpf::kServerBoxes;
+            const uint32_t step = crowd ? tpf::kServerBoxes / 4u : 1u;
+            for (uint32_t k = 0; k < tries; ++k)
             {
-                const uint32_t i = (hint + k) % tpf::kServerBoxes;
+                const uint32_t i = (hint + k * step) % tpf::kServerBoxes;
                 if (try_lease(i))
                     return static_cast<int>(i);
             }
-            // more callers than mailboxes: wait without burning CPU when crowded
-            if (crowded())
-                nap_ns(2000);
+            if (crowd)
+            {
+                box[hint].waiters.fetch_add(1u, std::memory_order_seq_cst);
+                box[hint].busy.wait(1u, std::memory_order_acquire); // returns at once if it is free by now
+                box[hint].waiters.fetch_sub(1u, std::memory_order_relaxed);
+            }
             else
                 std::this_thread::yield();
         }
     }
-    void release(int i) { box[i].busy.store(0u, std::memory_order_release); }
+    void release(int i)
+    {
+        box[i].busy.store(0u, std::memory_order_seq_cst);
+        if (box[i].waiters.load(std::memory_order_seq_cst) != 0u) // only with more callers than mailboxes
+            box[i].busy.notify_one();
+    }
     // the pause side: every mailbox, as the calls holding them return
     void hold_all()
     {
@@ -487,14 +501,18 @@ struct Server
         const bool crowd = crowded();
         const auto t0 = std::chrono::steady_clock::now();
         bool patient = false;
+        // crowded: a first nap of about one call's latency (most answers are
+        // in by then; every wake-up costs CPU time the callers share), later
+        // naps 2 us.  (A first nap tracking the thread's own latency fed back
+        // on itself -- the latency includes the nap -- and doubled it, r6h.)
         if (crowd)
-            nap_ns(3000);
+            nap_ns(4000);
         for (uint64_t spin = 1;; ++spin)
         {
             if (__atomic_load_n(&a->ack, __ATOMIC_ACQUIRE) == r)
                 break;
             if (crowd)
-                nap_ns(1000);
+                nap_ns(2000);
             else if (patient)
                 std::this_thread::yield();
             else
@@ -619,14 +637,8 @@ struct BoxLease
     tpf::ServerReq * rq;
     int i = 0;
     bool own = false;
-    bool gated = false;
     explicit BoxLease(Server & srv) : s(srv), rq(nullptr)
     {
-        if (t_pause_depth == 0 && callers() > tpf::kServerBoxes)
-        {
-            s.gate.acquire();
-            gated = true;
-        }
         if (t_pause_depth == 0)
             for (;;)
             {
@@ -644,8 +656,6 @@ struct BoxLease
     {
         if (own)
             s.release(i);
-        if (gated)
-            s.gate.release();
     }
     tpf::ServerReqBox * req() const { return &rq->box[i]; }
     tpf::ServerAnsBox * ans() const { return &s.an->box[i]; }

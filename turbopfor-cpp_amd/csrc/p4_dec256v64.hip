@@ -72,7 +72,7 @@ __device__ __forceinline__ uint64_t row16_sum64(uint64_t x)
 
 template <uint32_t WB>
 constexpr uint32_t kDsum64Lim = WB + 28u;
-static_assert(kDsum64Lim<16384u> / 4u + 5u <= (16384u + 64u) / 4u, "clamped phase-A reads stay in the wave's window");
+static_assert(kDsum64Lim<16384u> / 4u + 6u <= (16384u + 64u) / 4u, "clamped phase-A reads stay in the wave's window");
 
 template <uint32_t NB, uint32_t WB>
 __global__ __launch_bounds__(256, 2) void k_dsum128v64_lanes(const Dec64Args A)

@@ -86,6 +86,18 @@ __device__ __forceinline__ uint64_t base_sum4_lanes(const uint32_t * w, uint32_t
     return bs;
 }
 
+// vbGet64Inline's value (p4_scalar_internal.h:638-670) from its marker m and
+// the 8 bytes after it, D
+__device__ __forceinline__ uint64_t vb64_value(uint32_t m, uint64_t D)
+{
+    const uint32_t d = static_cast<uint32_t>(D);
+    const uint32_t v2 = ((m - 0x98u) << 8) + (d & 0xFFu) + 152u;
+    const uint32_t v3 = (d & 0xFFFFu) + ((m - 0xD8u) << 16) + 16536u;
+    const uint32_t nb = m - 0xF8u + 3u; // m >= 0xF8: 3..8 value bytes
+    const uint64_t vl = nb >= 8u ? D : (D & ((1ull << (8u * (nb & 7u))) - 1ull));
+    return m < 0x98u ? m : m < 0xD8u ? v2 : m < 0xF8u ? v3 : vl;
+}
+
 // Sum of one lane's 128v64 block at LDS byte p (act: the lane has a block
 // there).  Returns the block's byte length (wild for declined lanes); ok is
 // cleared when the lane path does not take the block.
@@ -150,18 +162,43 @@ __device__ __forceinline__ uint32_t dsum_block128v64_lanes(const uint32_t * w, u
     }
     if (__ballot(ok && comp) != 0ull)
     {
-        // the lane's own marker walk (vbGet64Inline, p4_scalar_internal.h:638-670)
+        // the lane's own marker walk (vbGet64Inline, p4_scalar_internal.h:638-670),
+        // two values per step (round 6; the 32-bit phase A's general walk): 24
+        // bytes from 6 aligned dwords, realigned to a[0..4] = bytes c..c+19;
+        // value 1 at offset 0, value 2 at value 1's length when that is <= 4
+        // (its 9 bytes then lie in a[0..4]; a longer first value takes the
+        // step alone).  One value per step cost 0.33 ms of the 1.45 ms phase A
+        // on the C3 64-bit list (r6h ablation).
         const bool on = ok && comp;
         uint32_t c = v0, k = 0u;
         while (__ballot(on && k < xn) != 0ull)
         {
-            const bool step = on && k < xn;
             const uint32_t cc = min(c, LIM);
-            const uint32_t by = lds_byte(w, cc);
-            const uint64_t v = vbyte_value<true>(w, cc, by);
-            exsum += step ? v : 0ull;
-            c += step ? vbyte_len<true>(by) : 0u;
-            k += step ? 1u : 0u;
+            const uint32_t q = cc >> 2, m = cc & 3u;
+            uint32_t d[6], a[5];
+#pragma unroll
+            for (uint32_t u = 0; u < 6u; ++u)
+                d[u] = w[q + u];
+#pragma unroll
+            for (uint32_t u = 0; u < 5u; ++u)
+                a[u] = __builtin_amdgcn_alignbyte(d[u + 1], d[u], m);
+            const bool s1 = on && k < xn;
+            const uint32_t by1 = a[0] & 0xFFu;
+            const uint32_t l1 = vbyte_len<true>(by1);
+            const uint64_t D1 = (static_cast<uint64_t>(__builtin_amdgcn_alignbyte(a[2], a[1], 1u)) << 32) |
+                                __builtin_amdgcn_alignbyte(a[1], a[0], 1u);
+            exsum += s1 ? vb64_value(by1, D1) : 0ull;
+            const bool hi1 = l1 >= 4u;
+            const uint32_t x0 = hi1 ? a[1] : a[0], x1 = hi1 ? a[2] : a[1], x2 = hi1 ? a[3] : a[2], x3 = hi1 ? a[4] : a[3];
+            const uint32_t r = l1 & 3u;
+            const uint32_t xw = __builtin_amdgcn_alignbyte(x1, x0, r), yw = __builtin_amdgcn_alignbyte(x2, x1, r),
+                           zw = __builtin_amdgcn_alignbyte(x3, x2, r);
+            const uint32_t by2 = xw & 0xFFu;
+            const uint64_t D2 = (static_cast<uint64_t>(__builtin_amdgcn_alignbyte(zw, yw, 1u)) << 32) | __builtin_amdgcn_alignbyte(yw, xw, 1u);
+            const bool s2v = s1 && k + 1u < xn && l1 <= 4u;
+            exsum += s2v ? vb64_value(by2, D2) : 0ull;
+            c += s1 ? l1 + (s2v ? vbyte_len<true>(by2) : 0u) : 0u;
+            k += s1 ? (s2v ? 2u : 1u) : 0u;
         }
         vend = comp ? c : vend;
     }
@@ -169,15 +206,28 @@ __device__ __forceinline__ uint32_t dsum_block128v64_lanes(const uint32_t * w, u
     // positions: strictly increasing (the reference ORs repeated ones) and < 128
     if (__ballot(ok && is_vb) != 0ull)
     {
+        // 16 positions per step from 5 aligned dwords (round 6, as the 32-bit
+        // phase A; one LDS byte read per position before)
         const bool on = ok && is_vb;
         const uint32_t kmax = uni(wave_max_u32(on ? xn : 0u));
+        const uint32_t m = vend & 3u;
         uint32_t prev = 0u;
         bool inc = true;
-        for (uint32_t k = 0; k < kmax; ++k)
+        for (uint32_t k0 = 0; k0 < kmax; k0 += 16u)
         {
-            const uint32_t pos = wbyte<LIM>(w, vend + k) + 1u; // 1..256: the first compares against 0
-            inc = inc && (!(on && k < xn) || (pos > prev && pos <= 128u));
-            prev = pos;
+            const uint32_t q = min(vend + k0, LIM) >> 2;
+            uint32_t d[5];
+#pragma unroll
+            for (uint32_t u = 0; u < 5u; ++u)
+                d[u] = w[q + u];
+#pragma unroll
+            for (uint32_t u = 0; u < 16u; ++u)
+            {
+                const uint32_t a = __builtin_amdgcn_alignbyte(d[(u >> 2) + 1], d[u >> 2], m);
+                const uint32_t pos = __builtin_amdgcn_ubfe(a, 8u * (u & 3u), 8u) + 1u; // 1..256: the first compares against 0
+                inc = inc && (!(on && k0 + u < xn) || (pos > prev && pos <= 128u));
+                prev = pos;
+            }
         }
         ok = ok && (!is_vb || inc);
         len = is_vb ? vend + xn - p : len;

@@ -183,11 +183,8 @@ __device__ __forceinline__ void plan_run(const Run & R, const uint32_t * in, con
 
 // Write a run: lane j of (szv, pwv, ov) = size, plan word and byte offset of
 // block R.first+j.  img: the wave's zeroed LDS image (left zeroed).  Round 6:
-// the blocks' layouts come from a run plane (enc_geo, one vector pass per
-// run) and the copy-out goes through one buffer descriptor per run
-// (RunCopyB): the per-block scalar work of round 5's form -- 136 SALU and 29
-// branches per C3 block against 141 VALU, on the CU's one scalar unit -- is
-// gone.
+// each block's layout from enc_geo, single-lane steps without exec masks,
+// the copy-out through one buffer descriptor per run (RunCopyB; p4_enc32.h).
 template <bool D1, int PROBE = 0, class Run>
 __device__ __forceinline__ void write_run(const Run & R, const uint32_t * in, const uint32_t * starts, uint32_t start0,
                                           uint32_t szv, uint32_t pwv, uint64_t ov, uint32_t * img, uint32_t * val,
@@ -226,7 +223,7 @@ __device__ __forceinline__ void write_run(const Run & R, const uint32_t * in, co
         // the layout from three values read per block (the plan word, size and
         // output byte), derived on the scalar unit: eighteen v_readlane of a
         // full run plane cost more VALU cycles and 19 VGPRs (6 waves per SIMD
-        // instead of 8) than the scalar derivation (r6c)
+        // instead of 7) than the scalar derivation (r6d)
         const EncGeo G = enc_geo(rl32(pwv, jj), rl32(szv, jj), rl32(rel, jj), lead);
         emit_block256_g<true>(img, val, G, v, t);
         wave_lds_sync();
@@ -323,11 +320,14 @@ hipError_t launch_twopass(const uint32_t * in, uint64_t nblocks, const uint32_t 
     const RunScanWs<uint64_t> rs = RunScanWs<uint64_t>::carve(static_cast<uint8_t *>(ws) + al256(nblocks * 4u), nruns);
     const uint64_t per_wg = 4ull * run;
     const uint32_t grid = static_cast<uint32_t>((nblocks + per_wg - 1) / per_wg);
-    if constexpr (PP != 0 || PW != 0)
+    if constexpr (PP != 0)
     {
         if (d1)
-            return hipErrorInvalidValue; // the probes measure the plain encoder only
+            return hipErrorInvalidValue; // the plan probe measures the plain encoder only
     }
+    // (the write probe runs after the real plan pass in either mode: with d1
+    // it copies the staged values into the D1 blocks' sizes, the data
+    // movement of the D1 write pass, round 6)
     if (d1)
         hipLaunchKernelGGL((dev::k_enc256v32_plan<true, 0, RD>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off,
                            plan, rs.tot);
@@ -341,7 +341,7 @@ hipError_t launch_twopass(const uint32_t * in, uint64_t nblocks, const uint32_t 
     if (e != hipSuccess)
         return e;
     if (d1)
-        hipLaunchKernelGGL((dev::k_enc256v32_write<true, 0, RD>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off,
+        hipLaunchKernelGGL((dev::k_enc256v32_write<true, PW, RD>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off,
                            plan, rs.pre, rs.tile, out, out_cap);
     else
         hipLaunchKernelGGL((dev::k_enc256v32_write<false, PW>), dim3(grid), dim3(256), 0, stream, in, nblocks, starts, start0, off, plan,

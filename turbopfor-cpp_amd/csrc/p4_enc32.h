@@ -526,20 +526,29 @@ __device__ __forceinline__ void copy_out_image16(const uint32_t * img, uint32_t 
 // below in round 6: the same chunking, addressed through one buffer
 // descriptor per run with the layout read per block.
 
-// ---- round 6: the write pass's control plane in lanes ------------------------
-// the D1 write pass issued 136 SALU + 29 branches per block
-// against 141 VALU.  A CU has one scalar unit for its four SIMDs (a wave64
-// VALU takes 2 cycles on one SIMD-32), so the scalar side bound the pass:
-// every block re-derived its layout (payload offset, image phase, header
-// bytes, copy-out chunk range, 64-bit destination) with scalar arithmetic
-// and wrapped each single-lane step in exec-mask sections.  As the decoder's
-// RunPlaneT (p4_dec_run.h) did for decoding, the layout of every block of a
-// wave run is now computed ONCE per run in vector lanes (lane j = block j)
-// and read per block with v_readlane; single-lane stores become stores from
-// every lane with unowned lanes sent to their own trash dword (LDS) or an
-// out-of-range buffer offset (HBM: the store is dropped), so they need no
-// exec mask; and the copy-out addresses the run's output through one buffer
-// descriptor with 32-bit offsets.
+// ---- round 6: the write pass with its scalar side cut ----------------------
+// VERDICT r5 #1 read the D1 write pass's 136 SALU + 29 branches per block
+// (against 141 VALU) as the CU's one scalar unit binding the pass: every block
+// re-derived its layout (payload offset, image phase, header bytes, copy-out
+// chunk range, 64-bit destination) with scalar arithmetic and wrapped each
+// single-lane step in an exec-mask section.  Round 6 cut the scalar side:
+//   * single-lane stores (headers, bitmap bytes, carried bytes, raw marker)
+//     are stores from every lane, unowned lanes sent to their own trash dword
+//     (LDS) or an out-of-range buffer offset (HBM: the store is dropped);
+//   * the copy-out addresses a run's output through ONE buffer descriptor
+//     with 32-bit offsets (RunCopyB), the chunk loop's stores need no mask;
+//   * a block's layout comes from three values read per block (plan word,
+//     size, output byte) by one closed-form derivation (enc_geo);
+//   * the rank scatter, the vbyte loop and the base packing test their
+//     bounds with nested wave-uniform branches (one test per C3 block).
+// Measured (profiles/r6_enc_counters.txt, r6 A/B): C3 write pass SALU 136 ->
+// 42 and branches 29 -> 19 per block, VALU level -- and the pass ~3% faster:
+// the scalar unit was not what bound it.  The C4 write pass runs at the time
+// of its own data-movement probe (the same loads and stores with the
+// building removed: 3.20 vs 3.22 ms per 10M blocks), C3's within ~15% of
+// the D1 probe.  A run plane in vector lanes read with 18
+// v_readlane per block (the decoder's RunPlaneT form) was slower than the
+// scalar derivation: +19 VGPRs (6 instead of 7 waves per SIMD) and more VALU.
 
 // Buffer offset that the hardware range check drops (stores) / zeroes (loads).
 constexpr uint32_t kOob = 0x80000000u;

@@ -119,7 +119,8 @@ int tpfm_enc256v32(int mode, const uint32_t * d_in, uint64_t nblocks, int d1, co
         case 1:
             return d1 ? -1 : tpfm::rc(enc256::launch_twopass<1, 0>(d_in, nblocks, nullptr, 0u, false, d_out, out_cap, d_off, d_ws, s));
         case 2:
-            return d1 ? -1 : tpfm::rc(enc256::launch_twopass<0, 2>(d_in, nblocks, nullptr, 0u, false, d_out, out_cap, d_off, d_ws, s));
+            // the write pass's data movement (D1 too: the real D1 plan's sizes)
+            return tpfm::rc(enc256::launch_twopass<0, 2>(d_in, nblocks, d_starts, start0, d1 != 0, d_out, out_cap, d_off, d_ws, s));
         case 3:
             return tpfm::rc(enc256::launch_twopass<0, 0>(d_in, nblocks, d_starts, start0, d1 != 0, d_out, out_cap, d_off, d_ws, s));
         case 4:
