@@ -243,8 +243,11 @@ __global__ __launch_bounds__(256) void k_block_server(ServerReq * rq, ServerAns 
     uint64_t pub_a = born;
     for (uint32_t polls = 0;; ++polls)
     {
-        // the whole request line in one read: lanes 0..7 hold its first 8 words
+        // the whole request line in one read: lanes 0..7 hold its first 8
+        // words; the launch's quit word is loaded beside it, so both arrive
+        // in one memory latency (checked below when no request came)
         const uint32_t word = t < 8u ? ld_sys(line + t) : 0u;
+        const uint32_t quit = ld_agent(&ctl->quit);
         const uint32_t r = rl32w(word, 0);
         if (r != last)
         {
@@ -311,7 +314,7 @@ __global__ __launch_bounds__(256) void k_block_server(ServerReq * rq, ServerAns 
         // mailboxes whose waves had gone).  The idle test (last_active) and
         // the host's stop word are read every 256th poll (each read of the
         // stop word crosses PCIe in mode 2).
-        if (uni(ld_agent(&ctl->quit)) != 0u)
+        if (uni(quit) != 0u)
             break;
         bool leave = __builtin_amdgcn_s_memrealtime() - born > max_ticks;
         if ((polls & 255u) == 0u)
