@@ -698,19 +698,10 @@ __device__ __forceinline__ void emit_block256_g(uint32_t * img, uint32_t * val, 
         pack_base_runs4<PAD>(img, G.pw, val, b, t);
         return;
     }
-    const bool f0 = v.x > m, f1 = v.y > m, f2 = v.z > m, f3 = v.w > m;
-    const uint32_t my = static_cast<uint32_t>(f0) | (static_cast<uint32_t>(f1) << 1) | (static_cast<uint32_t>(f2) << 2) |
-                        (static_cast<uint32_t>(f3) << 3);
-    const uint32_t cnt = __builtin_popcount(my);
-    // exceptions in elements < 4t: the four flag ballots counted below the
-    // lane (eight v_mbcnt; round 6: the wave scan of cnt took six dependent
-    // DPP steps with their wait states, plus the count's add chain)
-    const uint64_t B0 = __builtin_amdgcn_ballot_w64(f0), B1 = __builtin_amdgcn_ballot_w64(f1), B2 = __builtin_amdgcn_ballot_w64(f2),
-                   B3 = __builtin_amdgcn_ballot_w64(f3);
-    auto below = [](uint64_t B, uint32_t acc) {
-        return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(B >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(B), acc));
-    };
-    const uint32_t before = below(B3, below(B2, below(B1, below(B0, 0u))));
+    const uint32_t f0 = v.x > m, f1 = v.y > m, f2 = v.z > m, f3 = v.w > m;
+    const uint32_t my = f0 | (f1 << 1) | (f2 << 2) | (f3 << 3);
+    const uint32_t cnt = f0 + f1 + f2 + f3;
+    const uint32_t before = wave_incl_scan(cnt) - cnt; // exceptions in elements < 4t
     const uint32_t sh = b & 31u;
     const uint32_t ex[4] = {v.x >> sh, v.y >> sh, v.z >> sh, v.w >> sh};
     if (G.bx <= 32u)
