@@ -5,7 +5,11 @@
 //   dw   : lane t stores elements t and t+64 (two dword store instructions per block, k_dec_h32w)
 //   x4   : lane t stores elements 4t..4t+3 with one 16-byte store (4-byte aligned), the ragged
 //          last lane with dword stores
-//   Each with default and nt store policy.
+//   a16  : (round 6) the wave's whole output range (64 blocks x 508 B = 32,512 B, 16-byte aligned:
+//          the run starts at a multiple of 64 blocks) in 16-byte aligned chunks, one chunk per lane per
+//          store instruction -- the store pattern an LDS-staged output would issue, with the staging's
+//          own cost left out
+//   Each with default and nt store policy (a16 also sc1 nt).
 // Build: hipcc --offload-arch=gfx950 -O3 -o c1_store_probe c1_store_probe.hip
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -37,6 +41,8 @@ __global__ __launch_bounds__(256) void k_probe(const uint8_t * __restrict in, ui
     for (uint32_t jj = 0; jj < nr; ++jj)
     {
         const uint32_t v2 = v + jj;
+        if (MODE == 2)
+            break;
         if (MODE == 0)
         {
             __builtin_amdgcn_raw_buffer_store_b32(v2, os, static_cast<int>((jj * 127u + t) * 4u), 0, AUX);
@@ -51,6 +57,12 @@ __global__ __launch_bounds__(256) void k_probe(const uint8_t * __restrict in, ui
                 for (uint32_t i = 0; e + i < 127u; ++i)
                     __builtin_amdgcn_raw_buffer_store_b32(v2, os, static_cast<int>((jj * 127u + e + i) * 4u), 0, AUX);
         }
+    }
+    if (MODE == 2)
+    {
+        const uint32_t chunks = nr * 508u / 16u; // nr = 64: 2,032 whole chunks
+        for (uint32_t c = t; c < chunks; c += 64u)
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{v, v + c, v, v}, os, static_cast<int>(16u * c), 0, AUX);
     }
 }
 
@@ -86,6 +98,9 @@ int main()
         run("dw nt", [&] { k_probe<0, 2><<<grid, 256>>>(in, out, nblk); });
         run("x4", [&] { k_probe<1, 0><<<grid, 256>>>(in, out, nblk); });
         run("x4 nt", [&] { k_probe<1, 2><<<grid, 256>>>(in, out, nblk); });
+        run("a16", [&] { k_probe<2, 0><<<grid, 256>>>(in, out, nblk); });
+        run("a16 nt", [&] { k_probe<2, 2><<<grid, 256>>>(in, out, nblk); });
+        run("a16 sc1nt", [&] { k_probe<2, 18><<<grid, 256>>>(in, out, nblk); });
     }
     return 0;
 }
