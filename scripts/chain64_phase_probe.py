@@ -2,8 +2,9 @@
 tpf_d1dec64_chain_sums (phase A: k_dsum128v64_lanes + u64 run scan) and
 tpf_d1dec64_chain_decode (phase B: k_dec128v64w<2, Prefix>) timed separately
 with HIP events on the C3-as-u64 chained list of bench.py --workload
-c3chain64, plus the per-unit-starts decode of the same stream.  With
-TPF_LIB=ablib/x.so (A/B and ablation builds) the sums may be wrong: nothing is
+c3chain64, plus the per-unit-starts decode of the same stream and the
+decoder's data-movement probe on it (tpfm_probe256v64: its loads and stores,
+no decoding).  With TPF_LIB=ablib/x.so (A/B and ablation builds) the sums may be wrong: nothing is
 verified here.
 usage: TPF_LIB=... python scripts/chain64_phase_probe.py [nunits] [reps]"""
 import ctypes
@@ -45,8 +46,12 @@ def per_unit():
     tpf.dec_batch("256v64", packed, offs, nb, 256, starts=starts, out=out.view(-1))
 
 
+def probe():
+    tpf.probe256v64(packed, offs, nb, out.view(-1))
+
+
 res = {}
-for name, f in (("phaseA", a), ("phaseB", b), ("per_unit_starts", per_unit)):
+for name, f in (("phaseA", a), ("phaseB", b), ("per_unit_starts", per_unit), ("probe", probe)):
     f()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()

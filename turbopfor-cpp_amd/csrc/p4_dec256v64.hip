@@ -119,13 +119,11 @@ __global__ __launch_bounds__(256, 2) void k_dsum128v64_lanes(const Dec64Args A)
     {
         const uint64_t pbase = wbase;
         const uint32_t pspan = span;
+        // unconditional (round 6, as k_dsum256v32_lanes): chunks past the
+        // span hold the zeros their out-of-range loads returned
 #pragma unroll
         for (uint32_t i = 0; i < NL; ++i)
-        {
-            const uint32_t x = 16u * t + 1024u * i;
-            if (x < pspan)
-                reinterpret_cast<u32x4 *>(win)[x >> 4] = r[i];
-        }
+            reinterpret_cast<u32x4 *>(win)[(16u * t + 1024u * i) >> 4] = r[i];
         {
             const uint32_t xs = avail & ~15u;
             if (xs < pspan && (avail & 15u) != 0u && t == ((xs >> 4) & 63u))

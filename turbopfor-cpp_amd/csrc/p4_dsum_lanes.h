@@ -151,12 +151,15 @@ __device__ __forceinline__ uint32_t base_sum_lanes(const uint32_t * w, uint32_t 
     const uint32_t m = pay & 3u;
     uint32_t q = min(pay, LIM) >> 2;
     uint32_t phi = 0u, bs = 0u;
+    uint32_t d[9];
+    d[0] = w[q];
     for (uint32_t k = 0; k < bmax; ++k)
     {
         const uint32_t s = phi ? b - phi : 0u;
-        uint32_t d[9];
+        // d[0] is the previous word's d[8] (the same dword: q advances by 8
+        // and a valid lane's q is never clamped)
 #pragma unroll
-        for (uint32_t l = 0; l < 9u; ++l)
+        for (uint32_t l = 1; l < 9u; ++l)
             d[l] = w[q + l];
         // the 8 folded dwords summed in 64 bits (one add with carry each,
         // round 5): slots below T cannot carry into T, so the low T bits
@@ -185,6 +188,7 @@ __device__ __forceinline__ uint32_t base_sum_lanes(const uint32_t * w, uint32_t 
             lo = (lo & QA[lv]) + ((lo >> W[lv]) & QB[lv]);
         bs += on && k < b ? (firsts << phi) + lo + hi : 0u;
         q = min(q + 8u, LIM / 4u);
+        d[0] = d[8];
         phi += c32;
         phi = phi >= b ? phi - b : phi;
     }
@@ -290,40 +294,56 @@ __device__ __forceinline__ bool dsum_lanes(const uint32_t * w, uint32_t p, uint3
         bool fast = ok && comp && len >= hl + xn && lr >= xn && lr <= 64u;
         if (__ballot(fast) != 0ull)
         {
-            constexpr uint32_t QMAX = (LIM + 20u) / 4u;
+            // Round 6: the region's dwords q0 .. q0 + 16 (lr <= 64 bytes
+            // from byte m0 < 4 of dword q0) are read from one base pointer
+            // clamped once to QF, so that every read stays inside the wave's
+            // window ((LIM + 36) / 4 dwords); a valid lane's region ends
+            // inside [0, WB) = [0, LIM - 28), so its base is never clamped.
+            // The byte mask is one 64-bit shift, the carry between dwords two
+            // 32-bit adds, and the markers are counted by popcounts of whole
+            // 0xFF bytes (8 per marker).
+            constexpr uint32_t QF = (LIM + 36u) / 4u - 17u;
             const uint32_t jmax = uni(wave_max_u32(fast ? (lr + 3u) >> 2 : 0u));
-            const uint32_t q0 = min(v0, LIM) >> 2, m0 = v0 & 3u;
-            uint32_t dprev = w[q0];
-            uint32_t aprev = 0u, mprev = 0u, cin = 0u, tsum = 0u, s2 = 0u, n1 = 0u, n2 = 0u, bad = 0u;
-            for (uint32_t j = 0; j < jmax; ++j)
+            const uint32_t * wq = w + min(v0 >> 2, QF);
+            const uint32_t m0 = v0 & 3u, e8 = 8u * lr;
+            uint32_t dprev = wq[0];
+            uint32_t aprev = 0u, mprev = 0u, cin = 0u, tsum = 0u, s2 = 0u, nm8 = 0u, n28 = 0u, bad = 0u;
+#pragma unroll
+            for (uint32_t j = 0; j < 16u; ++j)
             {
-                const uint32_t dn = w[min(q0 + j + 1u, QMAX)];
+                if (j >= jmax)
+                    break;
+                const uint32_t dn = wq[j + 1u];
                 const uint32_t x = __builtin_amdgcn_alignbyte(dn, dprev, m0); // region bytes 4j..4j+3
                 dprev = dn;
-                const uint32_t rem = lr > 4u * j ? lr - 4u * j : 0u;
-                const uint32_t rm = rem >= 4u ? 0xFFFFFFFFu : mask32(8u * rem);
+                // the bytes of x inside the region: the low min(lr - 4j, 4) (clamped at 0)
+                const uint32_t sh = min(e8 > 32u * j ? e8 - 32u * j : 0u, 32u);
+                const uint32_t rm = static_cast<uint32_t>((0xFFFFFFFFull << sh) >> 32);
                 const uint32_t hi = x & 0x80808080u, y = x & 0x7F7F7F7Fu;
                 const uint32_t gedc = (y + 0x24242424u) & hi;                     // bytes >= 0xDC (bit 7)
                 const uint32_t a80 = (y + 0x64646464u) & hi & ~gedc;              // bytes in [0x9C, 0xDC)
                 const uint32_t am = a80 | (a80 - (a80 >> 7));                     // as 0xFF bytes
                 const uint32_t sha = __builtin_amdgcn_alignbyte(am, aprev, 3u);   // A of byte k-1
                 aprev = am;
-                const uint64_t xs = static_cast<uint64_t>(am) + ((am & ~sha) & 0x00010001u) + cin;
-                cin = static_cast<uint32_t>(xs >> 32);
-                const uint32_t re = am & ~static_cast<uint32_t>(xs);              // runs starting at even offsets
+                uint32_t c1, c2;
+                const uint32_t xs0 = __builtin_addc(am, (am & ~sha) & 0x00010001u, 0u, &c1);
+                const uint32_t xs = __builtin_addc(xs0, 0u, cin, &c2);
+                cin = c1 | c2;
+                const uint32_t re = am & ~xs;                                     // runs starting at even offsets
                 const uint32_t mr = (re & 0x00FF00FFu) | (am & ~re & 0xFF00FF00u); // markers inside runs
                 const uint32_t shm = __builtin_amdgcn_alignbyte(mr, mprev, 3u);
                 mprev = mr;
-                const uint32_t mk = (mr | ~(am | shm)) & rm;                     // every marker
-                const uint32_t ma = mk & am;
+                const uint32_t mk = (mr | ~(am | shm)) & rm;                     // every marker, as 0xFF bytes
+                const uint32_t ma = mk & am;                                      // the 2-byte markers
                 tsum = __builtin_amdgcn_sad_u8(x & rm, 0u, tsum);
                 s2 = __builtin_amdgcn_sad_u8(x & ma, 0u, s2);
-                n2 += __builtin_popcount(ma & 0x01010101u);
-                n1 += __builtin_popcount(mk & ~am & 0x01010101u);
+                nm8 += __builtin_popcount(mk);
+                n28 += __builtin_popcount(ma);
                 bad |= mk & gedc;
             }
-            fast = fast && bad == 0u && n1 + n2 == xn && n1 + 2u * n2 == lr;
-            exsum += fast ? tsum + 255u * s2 - 39780u * n2 : 0u;
+            // xn values (markers) in exactly lr bytes: n1 + n2 = xn, n1 + 2 n2 = lr
+            fast = fast && bad == 0u && nm8 == 8u * xn && 8u * xn + n28 == 8u * lr;
+            exsum += fast ? tsum + 255u * s2 - 39780u * (n28 >> 3) : 0u;
         }
         // The general walk (any vbyte lengths) for the other lanes.  The
         // marker chain is serial: each step reads 20 bytes at c (5 aligned
