@@ -445,8 +445,11 @@ struct Server
             }
             if (crowd)
             {
+                // seq_cst on both sides (the count, then the lock word here;
+                // the lock word, then the count in release): one of the two
+                // sees the other's store, so a release never skips a waiter
                 box[hint].waiters.fetch_add(1u, std::memory_order_seq_cst);
-                box[hint].busy.wait(1u, std::memory_order_acquire); // returns at once if it is free by now
+                box[hint].busy.wait(1u, std::memory_order_seq_cst); // returns at once if it is free by now
                 box[hint].waiters.fetch_sub(1u, std::memory_order_relaxed);
             }
             else
