@@ -132,10 +132,24 @@ __device__ __forceinline__ uint32_t dsum_block128v64_lanes(const uint32_t * w, u
         const bool on = ok && is_bm;
         const uint32_t kmax = uni(wave_max_u32(on ? pc : 0u));
         const uint32_t xs = (p + 18u) * 8u;
-        for (uint32_t k = 0; k < kmax; ++k)
+        if (__ballot(on && bx > 32u) == 0ull)
         {
-            const uint64_t v = lds_bits64(w, min(xs + k * bx, LIM * 8u), bx);
-            exsum += on && k < pc ? v : 0ull;
+            // every lane's exceptions fit 32 bits (round 6; the C3-as-u64 list:
+            // bx <= 12): one funnel read per exception -- lds_bits64's per-lane
+            // width tests cost two exec-mask sections per exception
+            for (uint32_t k = 0; k < kmax; ++k)
+            {
+                const uint32_t v = lds_bits(w, min(xs + k * bx, LIM * 8u), bx);
+                exsum += on && k < pc ? v : 0u;
+            }
+        }
+        else
+        {
+            for (uint32_t k = 0; k < kmax; ++k)
+            {
+                const uint64_t v = lds_bits64(w, min(xs + k * bx, LIM * 8u), bx);
+                exsum += on && k < pc ? v : 0ull;
+            }
         }
         len = is_bm ? 18u + xbytes + 16u * b : len;
         pay = is_bm ? p + 18u + xbytes : pay;

@@ -541,14 +541,15 @@ __device__ __forceinline__ void copy_out_image16(const uint32_t * img, uint32_t 
 //     size, output byte) by one closed-form derivation (enc_geo);
 //   * the rank scatter, the vbyte loop and the base packing test their
 //     bounds with nested wave-uniform branches (one test per C3 block).
-// Measured (profiles/r6_enc_counters.txt, r6 A/B): C3 write pass SALU 136 ->
-// 42 and branches 29 -> 19 per block, VALU level -- and the pass ~3% faster:
-// the scalar unit was not what bound it.  The C4 write pass runs at the time
-// of its own data-movement probe (the same loads and stores with the
-// building removed: 3.20 vs 3.22 ms per 10M blocks), C3's within ~15% of
-// the D1 probe.  A run plane in vector lanes read with 18
-// v_readlane per block (the decoder's RunPlaneT form) was slower than the
-// scalar derivation: +19 VGPRs (6 instead of 7 waves per SIMD) and more VALU.
+// Measured (profiles/r6_enc_counters.txt, r6 A/B), per C3 block: this form
+// issues 114 SALU + 128 VALU + 28.5 branches (round 5: 136 + 141 + 28.8); a
+// first round-6 form with the layouts in a run plane of vector lanes, read
+// with 18 v_readlane per block, issued 42 SALU + 144 VALU + 18.6 branches but
+// needed 19 more VGPRs (6 instead of 7 waves per SIMD) and ran slower.  Both
+// run the C3 write pass ~3% faster than round 5: the scalar unit was not
+// what bound it.  The C4 write pass runs at the time of its own data-movement
+// probe (the same loads and stores with the building removed: 3.13-3.19 vs
+// 3.10-3.22 ms per 10M blocks), C3's 19-25% above the D1 probe.
 
 // Buffer offset that the hardware range check drops (stores) / zeroes (loads).
 constexpr uint32_t kOob = 0x80000000u;
